@@ -1,0 +1,373 @@
+// a4/a5: LightGCN K-layer propagation -- CSR SpMM with the layer-sum / layer-mean fused into the
+// epilogue.
+//
+// Reference: LightGCN.computer() (lightGCN/LightGCN-PyTorch-master/code/model.py:145-177):
+//   all_emb = cat(user_w, item_w); K x all_emb = torch.sparse.mm(G, all_emb) (:171);
+//   embs = stack([E0..EK]) ; light_out = mean(embs, dim=1) (:173-175)
+// and the TF row-folded equivalent (LightGCN-tf/LightGCN.py:232-253).
+//
+// MI355X design (bandwidth-bound; no MFMA):
+//   * one G-lane group per row segment, G = row bytes / 16 rounded up to a power of two, so each
+//     lane moves exactly one 16-B chunk of every gathered embedding row (d=64 f32 or d=128 bf16:
+//     16 lanes, 4 rows per wave64);
+//   * the group loads G (col, val) pairs with one coalesced load each and broadcasts them with
+//     width-G shuffles, then issues UNROLL independent 16-B row gathers before the FMAs so every
+//     lane keeps several HBM/LLC requests in flight;
+//   * rows are cut into segments of <= seg_len nonzeros and scheduled longest-first (plan built
+//     host-side), so power-law hub rows neither serialise one group nor leave a tail; split rows
+//     reduce their fp32 partials in slot order in a fix-up pass (deterministic, no atomics);
+//   * the epilogue writes the next layer table AND folds the layer into the fp32 running sum, and
+//     the last layer writes the mean directly: the [K+1, N, d] stack of the reference is never
+//     materialised;
+//   * bf16 storage (LGX_DTYPE_BF16) halves the gathered bytes; arithmetic is fp32 throughout.
+#include "lgx_common.h"
+
+namespace lgx {
+namespace {
+
+constexpr int kThreads = 256;
+
+template <typename T>
+struct Vec;
+template <>
+struct Vec<float> {
+    static constexpr int N = 4;
+    typedef float4 raw;
+    __device__ static __forceinline__ void load(const float* p, float (&v)[4]) {
+        const float4 x = *reinterpret_cast<const float4*>(p);
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+    }
+    __device__ static __forceinline__ void store(float* p, const float (&v)[4]) {
+        *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+};
+template <>
+struct Vec<uint16_t> {
+    static constexpr int N = 8;
+    __device__ static __forceinline__ void load(const uint16_t* p, float (&v)[8]) {
+        const uint4 x = *reinterpret_cast<const uint4*>(p);
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            v[2 * j] = __uint_as_float(w[j] << 16);
+            v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+        }
+    }
+    __device__ static __forceinline__ void store(uint16_t* p, const float (&v)[8]) {
+        uint32_t w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            w[j] = (uint32_t)f32_to_bf16(v[2 * j]) | ((uint32_t)f32_to_bf16(v[2 * j + 1]) << 16);
+        *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+};
+
+struct LayerArgs {
+    const int64_t* indptr;
+    const int32_t* indices;
+    const float* vals;
+    const int32_t* seg_row;
+    const int32_t* seg_part;
+    const int32_t* seg_slot;
+    int64_t n_segs;
+    int64_t seg_len;
+    const int32_t* split_row;
+    const int32_t* split_ptr;
+    int64_t n_split;
+    float* partials;
+    const void* X;
+    void* Y;
+    const void* E0;
+    float* acc;
+    float* out;
+    int64_t d;
+    int mode;
+    float n_mean;
+};
+
+// finish one 16-B chunk (VEC values, columns [off, off+VEC)) of output row `row`
+template <typename T>
+__device__ __forceinline__ void finish_chunk(const LayerArgs& a, int64_t row, int64_t off,
+                                             float (&v)[Vec<T>::N]) {
+    constexpr int VEC = Vec<T>::N;
+    const int64_t o = row * a.d + off;
+    switch (a.mode) {
+        case LGX_LAYER_PLAIN:
+            Vec<T>::store(static_cast<T*>(a.Y) + o, v);
+            break;
+        case LGX_LAYER_FIRST: {
+            Vec<T>::store(static_cast<T*>(a.Y) + o, v);
+            float e[VEC];
+            Vec<T>::load(static_cast<const T*>(a.E0) + o, e);
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) e[j] += v[j];
+#pragma unroll
+            for (int j = 0; j < VEC; j += 4)
+                *reinterpret_cast<float4*>(a.acc + o + j) = make_float4(e[j], e[j + 1], e[j + 2], e[j + 3]);
+            break;
+        }
+        case LGX_LAYER_MID: {
+            Vec<T>::store(static_cast<T*>(a.Y) + o, v);
+#pragma unroll
+            for (int j = 0; j < VEC; j += 4) {
+                float4 s = *reinterpret_cast<const float4*>(a.acc + o + j);
+                s.x += v[j]; s.y += v[j + 1]; s.z += v[j + 2]; s.w += v[j + 3];
+                *reinterpret_cast<float4*>(a.acc + o + j) = s;
+            }
+            break;
+        }
+        case LGX_LAYER_LAST: {
+#pragma unroll
+            for (int j = 0; j < VEC; j += 4) {
+                float4 s = *reinterpret_cast<const float4*>(a.acc + o + j);
+                s.x = (s.x + v[j]) / a.n_mean;
+                s.y = (s.y + v[j + 1]) / a.n_mean;
+                s.z = (s.z + v[j + 2]) / a.n_mean;
+                s.w = (s.w + v[j + 3]) / a.n_mean;
+                *reinterpret_cast<float4*>(a.out + o + j) = s;
+            }
+            break;
+        }
+        default: {  // LGX_LAYER_ONLY
+            float e[VEC];
+            Vec<T>::load(static_cast<const T*>(a.E0) + o, e);
+#pragma unroll
+            for (int j = 0; j < VEC; j += 4)
+                *reinterpret_cast<float4*>(a.out + o + j) =
+                    make_float4((e[j] + v[j]) / a.n_mean, (e[j + 1] + v[j + 1]) / a.n_mean,
+                                (e[j + 2] + v[j + 2]) / a.n_mean, (e[j + 3] + v[j + 3]) / a.n_mean);
+            break;
+        }
+    }
+}
+
+template <typename T, int G, int CPL, int UNROLL>
+__global__ __launch_bounds__(kThreads) void spmm_segments(LayerArgs a) {
+    constexpr int VEC = Vec<T>::N;
+    const int gl = threadIdx.x & (G - 1);
+    const int64_t seg = (blockIdx.x * (int64_t)kThreads + threadIdx.x) / G;
+    if (seg >= a.n_segs) return;  // whole groups exit together (n_segs boundary is group-aligned)
+    const int64_t row = a.seg_row[seg];
+    const int part = a.seg_part[seg];
+    const int slot = a.seg_slot[seg];
+    const int64_t rb = a.indptr[row], re = a.indptr[row + 1];
+    const int64_t b = rb + (int64_t)part * a.seg_len;
+    const int64_t e = slot < 0 ? re : min(re, b + a.seg_len);
+    const T* __restrict__ X = static_cast<const T*>(a.X);
+    const int64_t d = a.d;
+
+    float acc[CPL][VEC];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c)
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) acc[c][j] = 0.0f;
+
+    for (int64_t base = b; base < e; base += G) {
+        const int n = (int)min((int64_t)G, e - base);
+        const int my_col = gl < n ? a.indices[base + gl] : 0;
+        const float my_val = gl < n ? a.vals[base + gl] : 0.0f;
+        for (int t = 0; t < n; t += UNROLL) {
+            float x[UNROLL][CPL][VEC];
+            float w[UNROLL];
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                const int src = t + u;  // group-uniform
+                const int col = __shfl(my_col, src < n ? src : 0, G);
+                w[u] = src < n ? __shfl(my_val, src, G) : 0.0f;
+                const T* xr = X + (int64_t)col * d;
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) {
+                    const int64_t off = (int64_t)(c * G + gl) * VEC;
+                    if (src < n && off < d) {
+                        Vec<T>::load(xr + off, x[u][c]);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < VEC; ++j) x[u][c][j] = 0.0f;
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+                for (int c = 0; c < CPL; ++c)
+#pragma unroll
+                    for (int j = 0; j < VEC; ++j) acc[c][j] = fmaf(w[u], x[u][c][j], acc[c][j]);
+        }
+    }
+
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+        const int64_t off = (int64_t)(c * G + gl) * VEC;
+        if (off >= d) continue;
+        if (slot >= 0) {
+            float* p = a.partials + (int64_t)slot * d + off;
+#pragma unroll
+            for (int j = 0; j < VEC; j += 4)
+                *reinterpret_cast<float4*>(p + j) = make_float4(acc[c][j], acc[c][j + 1], acc[c][j + 2], acc[c][j + 3]);
+        } else {
+            finish_chunk<T>(a, row, off, acc[c]);
+        }
+    }
+}
+
+// split rows: sum the segment partials in slot order, then the same epilogue
+template <typename T, int G, int CPL>
+__global__ __launch_bounds__(kThreads) void spmm_fixup(LayerArgs a) {
+    constexpr int VEC = Vec<T>::N;
+    const int gl = threadIdx.x & (G - 1);
+    const int64_t s = (blockIdx.x * (int64_t)kThreads + threadIdx.x) / G;
+    if (s >= a.n_split) return;
+    const int64_t row = a.split_row[s];
+    const int p0 = a.split_ptr[s], p1 = a.split_ptr[s + 1];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+        const int64_t off = (int64_t)(c * G + gl) * VEC;
+        if (off >= a.d) continue;
+        float v[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) v[j] = 0.0f;
+        for (int p = p0; p < p1; ++p) {
+            const float* q = a.partials + (int64_t)p * a.d + off;
+#pragma unroll
+            for (int j = 0; j < VEC; j += 4) {
+                const float4 t = *reinterpret_cast<const float4*>(q + j);
+                v[j] += t.x; v[j + 1] += t.y; v[j + 2] += t.z; v[j + 3] += t.w;
+            }
+        }
+        finish_chunk<T>(a, row, off, v);
+    }
+}
+
+template <typename T, int G, int CPL>
+int launch_layer(const LayerArgs& a, hipStream_t stream) {
+    constexpr int UNROLL = CPL == 1 ? 8 : (CPL == 2 ? 4 : 2);
+    constexpr int groups_per_block = kThreads / G;
+    if (a.n_segs > 0) {
+        const int64_t blocks = ceil_div(a.n_segs, groups_per_block);
+        spmm_segments<T, G, CPL, UNROLL><<<blocks, kThreads, 0, stream>>>(a);
+        LGX_LAUNCH_CHECK();
+    }
+    if (a.n_split > 0) {
+        const int64_t blocks = ceil_div(a.n_split, groups_per_block);
+        spmm_fixup<T, G, CPL><<<blocks, kThreads, 0, stream>>>(a);
+        LGX_LAUNCH_CHECK();
+    }
+    return LGX_OK;
+}
+
+template <typename T>
+int dispatch_layer(const LayerArgs& a, hipStream_t stream) {
+    constexpr int VEC = Vec<T>::N;
+    const int64_t chunks = a.d / VEC;
+    if (chunks <= 4) return launch_layer<T, 4, 1>(a, stream);
+    if (chunks <= 8) return launch_layer<T, 8, 1>(a, stream);
+    if (chunks <= 16) return launch_layer<T, 16, 1>(a, stream);
+    if (chunks <= 32) return launch_layer<T, 32, 1>(a, stream);
+    if (chunks <= 64) return launch_layer<T, 64, 1>(a, stream);
+    if (chunks <= 128) return launch_layer<T, 64, 2>(a, stream);
+    return launch_layer<T, 64, 4>(a, stream);
+}
+
+template <typename T>
+__global__ void to_f32_scaled(const T* __restrict__ src, float* __restrict__ dst, int64_t n) {
+    int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if constexpr (sizeof(T) == 4) dst[i] = src[i];
+    else dst[i] = bf16_to_f32(src[i]);
+}
+
+int check_csr(const lgx_csr* A, int64_t d, int dtype) {
+    LGX_REQUIRE(A && A->indptr, LGX_ERR_INVALID_ARG, "lgx: null CSR operator");
+    LGX_REQUIRE(dtype == LGX_DTYPE_F32 || dtype == LGX_DTYPE_BF16, LGX_ERR_INVALID_ARG,
+                "lgx: unknown dtype %d", dtype);
+    const int vec = dtype == LGX_DTYPE_F32 ? 4 : 8;
+    LGX_REQUIRE(d > 0 && d % vec == 0 && d <= 1024, LGX_ERR_UNSUPPORTED,
+                "lgx: embedding dim %lld must be a multiple of %d and <= 1024", (long long)d, vec);
+    LGX_REQUIRE(A->n_segs >= A->n_rows, LGX_ERR_INVALID_ARG,
+                "lgx: plan has %lld segments for %lld rows", (long long)A->n_segs, (long long)A->n_rows);
+    LGX_REQUIRE(A->seg_row && A->seg_part && A->seg_slot, LGX_ERR_INVALID_ARG, "lgx: CSR plan missing");
+    LGX_REQUIRE(A->n_split == 0 || (A->split_row && A->split_ptr && A->partials), LGX_ERR_INVALID_ARG,
+                "lgx: split rows need split_row / split_ptr / partials");
+    LGX_REQUIRE(A->seg_len > 0, LGX_ERR_INVALID_ARG, "lgx: seg_len must be > 0");
+    return LGX_OK;
+}
+
+}  // namespace
+}  // namespace lgx
+
+using namespace lgx;
+
+extern "C" int lgx_propagate_layer(const lgx_csr* A, const void* X, void* Y, const void* E0,
+                                   float* acc, float* out, int64_t d, int dtype, int mode,
+                                   float n_mean, lgx_stream_t stream) {
+    int rc = check_csr(A, d, dtype);
+    if (rc) return rc;
+    LGX_REQUIRE(mode >= LGX_LAYER_PLAIN && mode <= LGX_LAYER_ONLY, LGX_ERR_INVALID_ARG,
+                "lgx_propagate_layer: bad mode %d", mode);
+    LGX_REQUIRE(X || A->nnz == 0, LGX_ERR_INVALID_ARG, "lgx_propagate_layer: X is null");
+    const bool needY = mode <= LGX_LAYER_MID, needE0 = mode == LGX_LAYER_FIRST || mode == LGX_LAYER_ONLY;
+    const bool needAcc = mode >= LGX_LAYER_FIRST && mode <= LGX_LAYER_LAST;
+    const bool needOut = mode >= LGX_LAYER_LAST;
+    LGX_REQUIRE((!needY || Y) && (!needE0 || E0) && (!needAcc || acc) && (!needOut || out),
+                LGX_ERR_INVALID_ARG, "lgx_propagate_layer: missing buffer for mode %d", mode);
+    LGX_REQUIRE(!needOut || n_mean > 0.0f, LGX_ERR_INVALID_ARG, "lgx_propagate_layer: n_mean <= 0");
+    if (A->n_rows == 0) return LGX_OK;
+    LayerArgs a{A->indptr, A->indices, A->vals, A->seg_row, A->seg_part, A->seg_slot, A->n_segs,
+                A->seg_len, A->split_row, A->split_ptr, A->n_split, A->partials,
+                X, Y, E0, acc, out, d, mode, n_mean};
+    if (dtype == LGX_DTYPE_F32) return dispatch_layer<float>(a, as_hip(stream));
+    return dispatch_layer<uint16_t>(a, as_hip(stream));
+}
+
+extern "C" int lgx_spmm_csr(const lgx_csr* A, const void* X, void* Y, int64_t d, int dtype,
+                            lgx_stream_t stream) {
+    return lgx_propagate_layer(A, X, Y, nullptr, nullptr, nullptr, d, dtype, LGX_LAYER_PLAIN, 1.0f, stream);
+}
+
+extern "C" int lgx_propagate_workspace(int64_t n_rows, int64_t d, int dtype, size_t* ws_bytes) {
+    LGX_REQUIRE(ws_bytes && n_rows >= 0 && d > 0, LGX_ERR_INVALID_ARG, "lgx_propagate_workspace: bad args");
+    const size_t es = dtype == LGX_DTYPE_F32 ? 4 : 2;
+    *ws_bytes = 2 * align_up(n_rows * d * es) + align_up(n_rows * d * 4);
+    return LGX_OK;
+}
+
+extern "C" int lgx_propagate(const lgx_csr* A, const void* E0, float* out, int64_t d, int K,
+                             int dtype, void* ws, size_t ws_bytes, lgx_stream_t stream_) {
+    hipStream_t stream = as_hip(stream_);
+    int rc = check_csr(A, d, dtype);
+    if (rc) return rc;
+    LGX_REQUIRE(E0 && out && K >= 0, LGX_ERR_INVALID_ARG, "lgx_propagate: bad arguments");
+    LGX_REQUIRE(A->n_rows == A->n_cols, LGX_ERR_INVALID_ARG, "lgx_propagate: operator must be square");
+    const int64_t N = A->n_rows;
+    if (N == 0) return LGX_OK;
+    if (K == 0) {  // mean of the single layer E0
+        const int64_t n = N * d;
+        if (dtype == LGX_DTYPE_F32)
+            to_f32_scaled<float><<<ceil_div(n, 256), 256, 0, stream>>>(static_cast<const float*>(E0), out, n);
+        else
+            to_f32_scaled<uint16_t><<<ceil_div(n, 256), 256, 0, stream>>>(static_cast<const uint16_t*>(E0), out, n);
+        LGX_LAUNCH_CHECK();
+        return LGX_OK;
+    }
+    size_t need = 0;
+    lgx_propagate_workspace(N, d, dtype, &need);
+    LGX_REQUIRE(ws && ws_bytes >= need, LGX_ERR_WORKSPACE, "lgx_propagate: workspace %zu < %zu", ws_bytes, need);
+    const size_t es = dtype == LGX_DTYPE_F32 ? 4 : 2;
+    char* base = static_cast<char*>(ws);
+    void* buf[2] = {base, base + align_up(N * d * es)};
+    float* acc = reinterpret_cast<float*>(base + 2 * align_up(N * d * es));
+    const float n_mean = (float)(K + 1);
+    const void* X = E0;
+    for (int k = 1; k <= K; ++k) {
+        int mode;
+        if (K == 1) mode = LGX_LAYER_ONLY;
+        else if (k == 1) mode = LGX_LAYER_FIRST;
+        else if (k == K) mode = LGX_LAYER_LAST;
+        else mode = LGX_LAYER_MID;
+        void* Y = buf[k & 1];
+        rc = lgx_propagate_layer(A, X, Y, E0, acc, out, d, dtype, mode, n_mean, stream_);
+        if (rc) return rc;
+        X = Y;
+    }
+    return LGX_OK;
+}

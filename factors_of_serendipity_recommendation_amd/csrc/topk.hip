@@ -1,0 +1,119 @@
+// a9: row-wise top-k of a dense score matrix + a10: fold-out metric curves.
+//
+// Reference: c_top_k_index / c_top_k_array_index (LightGCN-tf/evaluator/cpp/include/tools.h:
+// 13-33: std::partial_sort_copy per row on a host thread pool) and evaluate_foldout
+// (evaluator/cpp/include/evaluate_foldout.h:16-195).
+//
+// One 256-thread workgroup per row: each of its 4 waves streams an interleaved quarter of the
+// row with coalesced 256-B loads, filters against its running k-th key and merges survivors with
+// the register bitonic network of wave_topk.h; wave 0 then merges the other three lists.
+#include "wave_topk.h"
+
+namespace lgx {
+namespace {
+
+constexpr int kWavesPerRow = 4;
+constexpr int kUnroll = 4;
+
+__global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict__ S, int64_t cols,
+                                                        int64_t ld, int k, int32_t* __restrict__ out_idx,
+                                                        float* __restrict__ out_val) {
+    __shared__ uint64_t lists[kWavesPerRow][kWave];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t row = blockIdx.x;
+    const float* s = S + row * ld;
+    uint64_t top = 0;
+    const int64_t stride = (int64_t)kWave * kWavesPerRow;
+    for (int64_t base = (int64_t)wave * kWave; base < cols; base += stride * kUnroll) {
+        uint64_t cand[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int64_t c = base + u * stride + lane;
+            cand[u] = c < cols ? make_key(s[c], (int32_t)c) : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) wave_topk_push(top, cand[u], k, lane);
+    }
+    lists[wave][lane] = top;
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+        for (int w = 1; w < kWavesPerRow; ++w) wave_topk_push(top, lists[w][lane], k, lane);
+        if (lane < k) {
+            out_idx[row * k + lane] = top ? key_index(top) : -1;
+            if (out_val) out_val[row * k + lane] = top ? key_score(top) : -INFINITY;
+        }
+    }
+}
+
+__device__ __forceinline__ bool in_list(const int32_t* t, int64_t n, int32_t x) {
+    for (int64_t j = 0; j < n; ++j)
+        if (t[j] == x) return true;
+    return false;
+}
+
+// evaluate_foldout.h:16-112 per user; float accumulators with double increments as in the C++.
+__global__ void foldout_kernel(const int32_t* __restrict__ rankings, int64_t users, int k,
+                               const int64_t* __restrict__ truth_indptr,
+                               const int32_t* __restrict__ truth_indices,
+                               const double* __restrict__ inv_log2, float* __restrict__ results) {
+    const int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (u >= users) return;
+    const int32_t* rank = rankings + u * k;
+    const int32_t* truth = truth_indices + truth_indptr[u];
+    const int64_t tl = truth_indptr[u + 1] - truth_indptr[u];
+    float* out = results + u * 5 * (int64_t)k;
+    int hits = 0;
+    float sum_pre = 0.0f, dcg = 0.0f, idcg = 0.0f;
+    bool found = false;
+    for (int i = 0; i < k; ++i) {
+        const bool hit = in_list(truth, tl, rank[i]);
+        if (hit) {
+            hits += 1;
+            const float pre = (float)(1.0 * hits / (i + 1));
+            sum_pre += pre;
+            dcg = (float)((double)dcg + inv_log2[i]);
+        }
+        if (i < tl) idcg = (float)((double)idcg + inv_log2[i]);
+        out[i] = (float)(1.0 * hits / (i + 1));
+        out[k + i] = (float)(1.0 * hits / (double)tl);
+        out[2 * k + i] = sum_pre / (float)tl;
+        out[3 * k + i] = dcg / idcg;
+        if (!found && hit) {
+            found = true;
+            const float rr = (float)(1.0 / (i + 1));
+            for (int j = i; j < k; ++j) out[4 * k + j] = rr;
+        } else if (!found) {
+            out[4 * k + i] = 0.0f;
+        }
+    }
+}
+
+}  // namespace
+}  // namespace lgx
+
+using namespace lgx;
+
+extern "C" int lgx_topk_rows(const float* S, int64_t rows, int64_t cols, int64_t ld, int k,
+                             int32_t* out_idx, float* out_val, lgx_stream_t stream) {
+    LGX_REQUIRE(rows >= 0 && cols >= 0 && ld >= cols && out_idx && (rows == 0 || S), LGX_ERR_INVALID_ARG,
+                "lgx_topk_rows: bad arguments");
+    LGX_REQUIRE(k >= 1 && k <= 64, LGX_ERR_UNSUPPORTED, "lgx_topk_rows: k=%d outside [1, 64]", k);
+    if (rows == 0) return LGX_OK;
+    topk_rows_kernel<<<rows, 256, 0, as_hip(stream)>>>(S, cols, ld, k, out_idx, out_val);
+    LGX_LAUNCH_CHECK();
+    return LGX_OK;
+}
+
+extern "C" int lgx_foldout_metrics(const int32_t* rankings, int64_t users, int k,
+                                   const int64_t* truth_indptr, const int32_t* truth_indices,
+                                   const double* inv_log2, float* results, lgx_stream_t stream) {
+    LGX_REQUIRE(users >= 0 && k >= 1, LGX_ERR_INVALID_ARG, "lgx_foldout_metrics: bad sizes");
+    if (users == 0) return LGX_OK;
+    LGX_REQUIRE(rankings && truth_indptr && inv_log2 && results, LGX_ERR_INVALID_ARG,
+                "lgx_foldout_metrics: null pointer");
+    foldout_kernel<<<ceil_div(users, 128), 128, 0, as_hip(stream)>>>(rankings, users, k, truth_indptr,
+                                                                      truth_indices, inv_log2, results);
+    LGX_LAUNCH_CHECK();
+    return LGX_OK;
+}

@@ -1,0 +1,110 @@
+"""Evaluation drop-ins: the PyTorch ``Procedure.Test`` loop, the TF ``batch_test.test`` loop and
+the C++ evaluator entry ``eval_score_matrix_foldout`` -- scoring, masking and top-k on the GPU.
+
+References:
+  Procedure.Test              lightGCN/LightGCN-PyTorch-master/code/Procedure.py:96-174
+  test_one_batch / metrics    Procedure.py:60-72, code/utils.py:218-285
+  batch_test.test             LightGCN-tf/utility/batch_test.py:25-84
+  eval_score_matrix_foldout   LightGCN-tf/evaluator/cpp/evaluate_foldout.py:12-18
+                              (-> apt_evaluate_foldout.pyx:22-65 -> tools.h + evaluate_foldout.h)
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence
+
+import numpy as np
+import torch
+
+from . import ops
+
+
+def eval_score_matrix_foldout(score_matrix, test_items, top_k: int = 20, thread_num=None) -> np.ndarray:
+    """Same signature/return as the reference: float32 [B, 5*top_k] = [pre|rec|ap|ndcg|mrr] curves.
+
+    ``thread_num`` is accepted for signature compatibility (the GPU needs no host thread pool)."""
+    if len(score_matrix) != len(test_items):
+        raise ValueError("The lengths of score_matrix and test_items are not equal.")
+    S = torch.as_tensor(np.ascontiguousarray(score_matrix, dtype=np.float32) if not torch.is_tensor(score_matrix)
+                        else score_matrix)
+    S = S.to(device="cuda", dtype=torch.float32).contiguous()
+    idx, _ = ops.topk_rows(S, top_k)
+    truth = ops.lists_to_device_csr(test_items, S.device, sort=False)
+    return ops.foldout_metrics(idx, truth).cpu().numpy()
+
+
+# --------------------------------------------------------------------------- PyTorch Test metrics
+def _label(test_data: Sequence[Sequence[int]], pred: np.ndarray) -> np.ndarray:
+    """utils.getLabel (code/utils.py:277-285)."""
+    r = []
+    for i in range(len(test_data)):
+        gt = set(int(x) for x in test_data[i])
+        r.append(np.array([int(x) in gt for x in pred[i]], dtype=float))
+    return np.array(r).astype("float")
+
+
+def test_one_batch(rating_k: np.ndarray, ground_true: Sequence[Sequence[int]], topks: Sequence[int]) -> Dict:
+    """Procedure.test_one_batch (Procedure.py:60-72) with RecallPrecision_ATk / NDCGatK_r."""
+    r = _label(ground_true, rating_k)
+    pre, rec, ndcg = [], [], []
+    recall_n = np.array([len(ground_true[i]) for i in range(len(ground_true))])
+    for k in topks:
+        right = r[:, :k].sum(1)
+        rec.append(np.sum(right / recall_n))
+        pre.append(np.sum(right) / k)
+        tm = np.zeros((len(r), k))
+        for i, items in enumerate(ground_true):
+            tm[i, :min(k, len(items))] = 1
+        idcg = np.sum(tm * 1. / np.log2(np.arange(2, k + 2)), axis=1)
+        dcg = np.sum(r[:, :k] * (1. / np.log2(np.arange(2, k + 2))), axis=1)
+        idcg[idcg == 0.] = 1.
+        nd = dcg / idcg
+        nd[np.isnan(nd)] = 0.
+        ndcg.append(np.sum(nd))
+    return {"recall": np.array(rec), "precision": np.array(pre), "ndcg": np.array(ndcg)}
+
+
+def Test(dataset, Recmodel, epoch=0, w=None, multicore=0, topks: Sequence[int] = (20,)) -> Dict:
+    """Procedure.Test on the fused engine: one propagation, one fused score+mask+top-k launch for
+    all test users (sigmoid scores, positives set to -(1<<10) as Procedure.py:134)."""
+    testDict: Dict[int, List[int]] = dataset.testDict
+    Recmodel = Recmodel.eval()
+    max_K = max(topks)
+    results = {"precision": np.zeros(len(topks)), "recall": np.zeros(len(topks)), "ndcg": np.zeros(len(topks))}
+    with torch.no_grad():
+        users = list(testDict.keys())
+        all_users, all_items = Recmodel.computer()
+        dev = all_users.device
+        allPos = dataset.getUserPosItems(users)
+        mask = ops.lists_to_device_csr(allPos, dev, sort=True)
+        rows = torch.as_tensor(users, dtype=torch.int64, device=dev)
+        idx, _ = ops.score_topk(all_users, all_items, max_K, user_rows=rows, mask=mask,
+                                mask_value=-float(1 << 10), apply_sigmoid=True)
+        rating_k = idx.cpu().numpy()
+        res = test_one_batch(rating_k, [testDict[u] for u in users], topks)
+        for key in results:
+            results[key] = res[key] / float(len(users))
+    return results
+
+
+# --------------------------------------------------------------------------- TF batch_test
+def batch_test(user_emb: torch.Tensor, item_emb: torch.Tensor, users_to_test: Sequence[int],
+               train_items: Dict[int, Sequence[int]], test_set: Dict[int, Sequence[int]],
+               Ks: Sequence[int] = (20,), train_set_flag: int = 0) -> Dict:
+    """batch_test.test (batch_test.py:25-84): raw dot-product ratings, training items set to -inf
+    (train_set_flag=0), top-max(Ks), fold-out curves, mean over users."""
+    top_show = np.sort(np.asarray(Ks))
+    max_top = int(max(top_show))
+    dev = user_emb.device
+    users = [int(u) for u in users_to_test]
+    rows = torch.as_tensor(users, dtype=torch.int64, device=dev)
+    if train_set_flag == 0:
+        truths = [test_set[u] for u in users]
+        mask = ops.lists_to_device_csr([train_items.get(u, []) for u in users], dev, sort=True)
+    else:
+        truths = [train_items[u] for u in users]
+        mask = None
+    idx, _ = ops.score_topk(user_emb, item_emb, max_top, user_rows=rows, mask=mask, mask_value=float("-inf"))
+    curves = ops.foldout_metrics(idx, ops.lists_to_device_csr(truths, dev, sort=False)).cpu().numpy()
+    final = np.mean(curves, axis=0).reshape(5, max_top)[:, top_show - 1].reshape(5, len(top_show))
+    return {"precision": final[0].astype(np.float64), "recall": final[1].astype(np.float64),
+            "ndcg": final[3].astype(np.float64)}

@@ -1,0 +1,247 @@
+"""Normalized-adjacency CSR graphs in HBM and their SpMM launch plans.
+
+Replaces the reference's host-side graph build (``Loader.getSparseGraph``,
+lightGCN/LightGCN-PyTorch-master/code/dataloader.py:339-376, and ``Data.get_adj_mat``,
+LightGCN-tf/utility/load_data.py:77-106): the edge list is uploaded once and the whole
+``D^-1/2 A D^-1/2`` CSR is built on the GPU (``lgx_build_norm_adj``).
+
+HBM layout of a ``CSRGraph`` (N = n_users + n_items rows; users first, then items, exactly the
+row order of the reference's ``cat([users_emb, items_emb])`` at model.py:151):
+    indptr  int64 [N+1]      indices int32 [nnz]      vals float32 [nnz]
+plus the launch plan of ``make_plan`` (segment tables, int32) and an fp32 partial-sum scratch.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+
+# Target number of row segments per launch: enough 16-lane groups to fill 256 CUs x 32 waves x 4.
+_TARGET_SEGMENTS = 65536
+
+
+def choose_seg_len(nnz: int) -> int:
+    """Segment length: long enough to amortise the fix-up, short enough that hub rows are split
+    into >= the chip's group slots (power of two in [64, 2048])."""
+    want = max(1, nnz // _TARGET_SEGMENTS)
+    s = 64
+    while s < want and s < 2048:
+        s *= 2
+    return s
+
+
+@dataclass
+class Plan:
+    """Host-side (numpy) launch plan; see ``struct lgx_csr`` in include/lgx.h."""
+
+    seg_row: np.ndarray
+    seg_part: np.ndarray
+    seg_slot: np.ndarray
+    split_row: np.ndarray
+    split_ptr: np.ndarray
+    seg_len: int
+
+    @property
+    def n_partials(self) -> int:
+        return int(self.split_ptr[-1]) if len(self.split_ptr) else 0
+
+
+def make_plan(indptr: np.ndarray, seg_len: Optional[int] = None) -> Plan:
+    """Cut every row into segments of <= seg_len nonzeros (every row, even an empty one, gets at
+    least one segment because its epilogue must still run) and order them longest-first so that
+    groups of one wave see similar trip counts and hub rows start early."""
+    indptr = np.asarray(indptr, dtype=np.int64)
+    lens = np.diff(indptr)
+    nnz = int(indptr[-1]) if len(indptr) else 0
+    if seg_len is None:
+        seg_len = choose_seg_len(nnz)
+    nseg = np.maximum(1, -(-lens // seg_len)).astype(np.int64)
+    order = np.argsort(-lens, kind="stable")
+    nseg_o = nseg[order]
+    total = int(nseg_o.sum())
+    if total >= 2**31:
+        raise ValueError("too many row segments for int32 plan tables")
+    seg_row = np.repeat(order, nseg_o).astype(np.int32)
+    starts = np.cumsum(nseg_o) - nseg_o
+    seg_part = (np.arange(total, dtype=np.int64) - np.repeat(starts, nseg_o)).astype(np.int32)
+    split_mask = nseg_o > 1
+    split_row = order[split_mask].astype(np.int32)
+    split_counts = nseg_o[split_mask]
+    split_ptr = np.zeros(len(split_row) + 1, dtype=np.int64)
+    np.cumsum(split_counts, out=split_ptr[1:])
+    slot_base = np.full(len(lens), -1, dtype=np.int64)
+    slot_base[split_row] = split_ptr[:-1]
+    seg_slot = np.where(nseg[seg_row] > 1, slot_base[seg_row] + seg_part, -1).astype(np.int32)
+    return Plan(seg_row, seg_part, seg_slot, split_row, split_ptr.astype(np.int32), int(seg_len))
+
+
+@dataclass
+class CSRGraph:
+    """A row block of the normalized adjacency resident in HBM, ready for ``lgx_propagate*``.
+
+    ``n_rows`` output rows; column ids index a table of ``n_cols`` rows.  For the single-GPU
+    operator n_rows == n_cols == n_users + n_items."""
+
+    indptr: torch.Tensor
+    indices: torch.Tensor
+    vals: torch.Tensor
+    n_rows: int
+    n_cols: int
+    n_users: int = 0
+    n_items: int = 0
+    plan: Optional[Plan] = None
+    _dev_plan: dict = field(default_factory=dict, repr=False)
+
+    @property
+    def nnz(self) -> int:
+        return int(self.indices.numel())
+
+    @property
+    def device(self) -> torch.device:
+        return self.indptr.device
+
+    def ensure_plan(self, seg_len: Optional[int] = None) -> "CSRGraph":
+        if self.plan is None or (seg_len is not None and seg_len != self.plan.seg_len):
+            self.plan = make_plan(self.indptr.cpu().numpy(), seg_len)
+            self._dev_plan.clear()
+        if not self._dev_plan:
+            dev = self.device
+            p = self.plan
+            self._dev_plan = {
+                "seg_row": torch.from_numpy(p.seg_row).to(dev),
+                "seg_part": torch.from_numpy(p.seg_part).to(dev),
+                "seg_slot": torch.from_numpy(p.seg_slot).to(dev),
+                "split_row": torch.from_numpy(p.split_row).to(dev),
+                "split_ptr": torch.from_numpy(p.split_ptr).to(dev),
+            }
+        return self
+
+    def partials(self, d: int) -> Optional[torch.Tensor]:
+        self.ensure_plan()
+        n = self.plan.n_partials
+        if n == 0:
+            return None
+        key = ("partials", d)
+        t = self._dev_plan.get(key)
+        if t is None:
+            t = torch.empty((n, d), dtype=torch.float32, device=self.device)
+            self._dev_plan[key] = t
+        return t
+
+    def c_struct(self, d: int) -> _lib.LgxCSR:
+        """``struct lgx_csr`` view (device pointers) for an embedding dim d."""
+        self.ensure_plan()
+        p, dp = self.plan, self._dev_plan
+        part = self.partials(d)
+        return _lib.LgxCSR(
+            self.indptr.data_ptr(), self.indices.data_ptr(), self.vals.data_ptr(),
+            self.n_rows, self.n_cols, self.nnz,
+            dp["seg_row"].data_ptr(), dp["seg_part"].data_ptr(), dp["seg_slot"].data_ptr(),
+            len(p.seg_row), p.seg_len,
+            dp["split_row"].data_ptr() if len(p.split_row) else None,
+            dp["split_ptr"].data_ptr(),
+            len(p.split_row), p.n_partials,
+            part.data_ptr() if part is not None else None,
+        )
+
+    def to_sparse_coo(self) -> torch.Tensor:
+        """The reference's graph object: a coalesced float32 torch sparse COO [N, N] on the same
+        device (dataloader.py:331-337, 373-374)."""
+        rows = torch.repeat_interleave(torch.arange(self.n_rows, device=self.device),
+                                       torch.diff(self.indptr))
+        idx = torch.stack([rows, self.indices.long()])
+        return torch.sparse_coo_tensor(idx, self.vals, (self.n_rows, self.n_cols)).coalesce()
+
+    def to_scipy(self):
+        import scipy.sparse as sp
+        return sp.csr_matrix((self.vals.cpu().numpy(), self.indices.cpu().numpy(),
+                              self.indptr.cpu().numpy()), shape=(self.n_rows, self.n_cols))
+
+
+def _stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_gpu(*tensors: torch.Tensor) -> None:
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("factors_of_serendipity_recommendation_amd ops run on the GPU only "
+                               f"(got a tensor on {t.device}); there is no CPU fallback")
+
+
+def build_norm_adj(users, items, n_users: int, n_items: int, dedup: bool = False,
+                   device="cuda", seg_len: Optional[int] = None) -> CSRGraph:
+    """D^-1/2 A D^-1/2 of the bipartite graph on the GPU (``lgx_build_norm_adj``).
+
+    dedup=False: duplicate (u,i) pairs are summed (PyTorch Loader, dataloader.py:288);
+    dedup=True: they collapse to one edge (TF Data, load_data.py:61)."""
+    device = torch.device(device)
+    u = torch.as_tensor(users).to(device=device, dtype=torch.int32).contiguous()
+    i = torch.as_tensor(items).to(device=device, dtype=torch.int32).contiguous()
+    require_gpu(u, i)
+    E = int(u.numel())
+    if int(i.numel()) != E:
+        raise ValueError("users and items must have the same length")
+    if E:
+        lo_u, hi_u = int(u.min()), int(u.max())
+        lo_i, hi_i = int(i.min()), int(i.max())
+        if lo_u < 0 or hi_u >= n_users or lo_i < 0 or hi_i >= n_items:
+            raise ValueError("edge index out of range")
+    N = n_users + n_items
+    L = _lib.lib()
+    ws = ctypes.c_size_t(0)
+    _lib.check(L.lgx_build_norm_adj_workspace(E, n_users, n_items, ctypes.byref(ws)),
+               "lgx_build_norm_adj_workspace")
+    indptr = torch.empty(N + 1, dtype=torch.int64, device=device)
+    indices = torch.empty(max(2 * E, 1), dtype=torch.int32, device=device)
+    vals = torch.empty(max(2 * E, 1), dtype=torch.float32, device=device)
+    work = torch.empty(max(ws.value, 1), dtype=torch.uint8, device=device)
+    _lib.check(L.lgx_build_norm_adj(u.data_ptr(), i.data_ptr(), E, n_users, n_items, int(dedup),
+                                    indptr.data_ptr(), indices.data_ptr(), vals.data_ptr(),
+                                    work.data_ptr(), ws.value, _stream_ptr(device)),
+               "lgx_build_norm_adj")
+    del work
+    nnz = int(indptr[-1].item())
+    g = CSRGraph(indptr, indices[:nnz], vals[:nnz], N, N, n_users, n_items)
+    g.ensure_plan(seg_len)
+    return g
+
+
+def from_csr_arrays(indptr, indices, vals, n_cols: Optional[int] = None, device="cuda",
+                    n_users: int = 0, n_items: int = 0, seg_len: Optional[int] = None) -> CSRGraph:
+    """Wrap existing CSR arrays (e.g. a loaded ``s_pre_adj_mat.npz``) as a device CSRGraph."""
+    device = torch.device(device)
+    ip = torch.as_tensor(np.asarray(indptr, dtype=np.int64) if not torch.is_tensor(indptr) else indptr)
+    ip = ip.to(device=device, dtype=torch.int64).contiguous()
+    ix = torch.as_tensor(indices).to(device=device, dtype=torch.int32).contiguous()
+    vv = torch.as_tensor(vals).to(device=device, dtype=torch.float32).contiguous()
+    require_gpu(ip)
+    n_rows = ip.numel() - 1
+    g = CSRGraph(ip, ix, vv, n_rows, n_cols if n_cols is not None else n_rows, n_users, n_items)
+    g.ensure_plan(seg_len)
+    return g
+
+
+def from_sparse_coo(G: torch.Tensor, n_users: int = 0, n_items: int = 0,
+                    seg_len: Optional[int] = None) -> CSRGraph:
+    """Accept the reference's graph (a coalesced torch sparse COO, dataloader.py:373-374) and
+    derive the CSR row pointer on the GPU (``lgx_csr_from_coo_rows``)."""
+    if not G.is_sparse:
+        raise TypeError("expected a torch sparse COO tensor")
+    G = G.coalesce()
+    require_gpu(G)
+    idx = G.indices()
+    rows = idx[0].contiguous()
+    n_rows, n_cols = G.shape
+    indptr = torch.empty(n_rows + 1, dtype=torch.int64, device=G.device)
+    _lib.check(_lib.lib().lgx_csr_from_coo_rows(rows.data_ptr(), rows.numel(), n_rows, indptr.data_ptr(),
+                                                _stream_ptr(G.device)), "lgx_csr_from_coo_rows")
+    g = CSRGraph(indptr, idx[1].to(torch.int32).contiguous(), G.values().to(torch.float32).contiguous(),
+                 n_rows, n_cols, n_users, n_items)
+    g.ensure_plan(seg_len)
+    return g

@@ -1,0 +1,195 @@
+"""Tensor-level wrappers over the liblgx C ABI (all GPU, stream-ordered on torch's current stream).
+
+Every function validates shapes/devices on the host, allocates outputs + workspace through torch's
+caching allocator and calls exactly one C entry point; no computation happens in Python and there
+is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib
+from .graph import CSRGraph, _stream_ptr, require_gpu
+
+_DT = {torch.float32: _lib.LGX_DTYPE_F32, torch.bfloat16: _lib.LGX_DTYPE_BF16}
+
+
+def _dtype_code(t: torch.Tensor) -> int:
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported embedding dtype {t.dtype}; use float32 or bfloat16") from None
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return t.data_ptr() if t is not None else None
+
+
+# ------------------------------------------------------------------------------------ propagation
+def propagate_layer(A: CSRGraph, X: torch.Tensor, mode: int, Y: Optional[torch.Tensor] = None,
+                    E0: Optional[torch.Tensor] = None, acc: Optional[torch.Tensor] = None,
+                    out: Optional[torch.Tensor] = None, n_mean: float = 1.0) -> None:
+    """One LightGCN layer (``lgx_propagate_layer``), writing into caller-provided buffers."""
+    require_gpu(X)
+    d = X.shape[1]
+    cs = A.c_struct(d)
+    _lib.check(_lib.lib().lgx_propagate_layer(ctypes.byref(cs), _ptr(X), _ptr(Y), _ptr(E0), _ptr(acc), _ptr(out),
+                                              d, _dtype_code(X), mode, float(n_mean), _stream_ptr(X.device)),
+               "lgx_propagate_layer")
+
+
+def spmm(A: CSRGraph, X: torch.Tensor) -> torch.Tensor:
+    """Y = A X (the reference's ``torch.sparse.mm(G, all_emb)``, model.py:171)."""
+    require_gpu(X)
+    X = X.contiguous()
+    if X.shape[0] != A.n_cols:
+        raise ValueError(f"X has {X.shape[0]} rows, operator has {A.n_cols} columns")
+    Y = torch.empty((A.n_rows, X.shape[1]), dtype=X.dtype, device=X.device)
+    cs = A.c_struct(X.shape[1])
+    _lib.check(_lib.lib().lgx_spmm_csr(ctypes.byref(cs), X.data_ptr(), Y.data_ptr(), X.shape[1], _dtype_code(X),
+                                       _stream_ptr(X.device)), "lgx_spmm_csr")
+    return Y
+
+
+def propagate(A: CSRGraph, E0: torch.Tensor, K: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """LightGCN.computer() body (model.py:149-175): mean over [E0, A E0, ..., A^K E0] -> fp32 [N, d].
+
+    E0 may be float32 or bfloat16 (bf16 storage, fp32 accumulation)."""
+    require_gpu(E0)
+    E0 = E0.contiguous()
+    N, d = E0.shape
+    if N != A.n_rows or A.n_rows != A.n_cols:
+        raise ValueError("propagate needs a square operator matching E0")
+    if out is None:
+        out = torch.empty((N, d), dtype=torch.float32, device=E0.device)
+    L = _lib.lib()
+    dt = _dtype_code(E0)
+    ws = ctypes.c_size_t(0)
+    _lib.check(L.lgx_propagate_workspace(N, d, dt, ctypes.byref(ws)), "lgx_propagate_workspace")
+    work = torch.empty(max(ws.value, 1), dtype=torch.uint8, device=E0.device)
+    cs = A.c_struct(d)
+    _lib.check(L.lgx_propagate(ctypes.byref(cs), E0.data_ptr(), out.data_ptr(), d, int(K), dt, work.data_ptr(),
+                               ws.value, _stream_ptr(E0.device)), "lgx_propagate")
+    return out
+
+
+# ------------------------------------------------------------------------------------ scoring
+def score_dense(Q: torch.Tensor, items: torch.Tensor, user_rows: Optional[torch.Tensor] = None,
+                apply_sigmoid: bool = False) -> torch.Tensor:
+    """[B, I] scores (getUsersRating, model.py:179-184 / TF batch_ratings, LightGCN.py:148)."""
+    require_gpu(Q, items, user_rows)
+    if Q.dtype != items.dtype:
+        raise TypeError("Q and items must share a dtype")
+    Q = Q.contiguous()
+    items = items.contiguous()
+    B = user_rows.numel() if user_rows is not None else Q.shape[0]
+    rows = user_rows.to(torch.int64).contiguous() if user_rows is not None else None
+    out = torch.empty((B, items.shape[0]), dtype=torch.float32, device=Q.device)
+    _lib.check(_lib.lib().lgx_score_dense(Q.data_ptr(), _ptr(rows), items.data_ptr(), B, items.shape[0], Q.shape[1],
+                                          _dtype_code(Q), int(apply_sigmoid), out.data_ptr(),
+                                          _stream_ptr(Q.device)), "lgx_score_dense")
+    return out
+
+
+def lists_to_device_csr(lists: Sequence[Sequence[int]], device, sort: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Ragged python lists -> (indptr int64 [n+1], indices int32) on the device."""
+    import numpy as np
+    lens = np.fromiter((len(l) for l in lists), dtype=np.int64, count=len(lists))
+    indptr = np.zeros(len(lists) + 1, dtype=np.int64)
+    np.cumsum(lens, out=indptr[1:])
+    if indptr[-1]:
+        parts = [np.asarray(l, dtype=np.int32) for l in lists]
+        if sort:
+            parts = [np.sort(p) for p in parts]
+        flat = np.concatenate(parts).astype(np.int32)
+    else:
+        flat = np.zeros(1, dtype=np.int32)
+    return torch.from_numpy(indptr).to(device), torch.from_numpy(flat).to(device)
+
+
+def score_topk(Q: torch.Tensor, items: torch.Tensor, k: int, user_rows: Optional[torch.Tensor] = None,
+               mask: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, mask_value: float = float("-inf"),
+               apply_sigmoid: bool = False, want_minmax: bool = False):
+    """Fused full-catalog score + positive mask + top-k (``lgx_score_topk``).
+
+    mask = (indptr int64 [B+1], indices int32) with each row's excluded items SORTED ascending.
+    Returns (idx int32 [B,k], val f32 [B,k]) or (idx, val, minmax f32[2])."""
+    require_gpu(Q, items, user_rows)
+    if Q.dtype != items.dtype:
+        raise TypeError("Q and items must share a dtype")
+    Q = Q.contiguous()
+    items = items.contiguous()
+    B = user_rows.numel() if user_rows is not None else Q.shape[0]
+    rows = user_rows.to(torch.int64).contiguous() if user_rows is not None else None
+    dev = Q.device
+    idx = torch.empty((B, k), dtype=torch.int32, device=dev)
+    val = torch.empty((B, k), dtype=torch.float32, device=dev)
+    mm = torch.empty(2, dtype=torch.float32, device=dev) if want_minmax else None
+    L = _lib.lib()
+    ws = ctypes.c_size_t(0)
+    _lib.check(L.lgx_score_topk_workspace(B, items.shape[0], k, ctypes.byref(ws)), "lgx_score_topk_workspace")
+    work = torch.empty(max(ws.value, 1), dtype=torch.uint8, device=dev)
+    mi, mx = (mask[0].contiguous(), mask[1].contiguous()) if mask is not None else (None, None)
+    if mi is not None and mi.numel() != B + 1:
+        raise ValueError("mask indptr must have B+1 entries")
+    _lib.check(L.lgx_score_topk(Q.data_ptr(), _ptr(rows), items.data_ptr(), B, items.shape[0], Q.shape[1],
+                                _dtype_code(Q), _ptr(mi), _ptr(mx), int(k), float(mask_value), int(apply_sigmoid),
+                                idx.data_ptr(), val.data_ptr(), _ptr(mm), work.data_ptr(), ws.value,
+                                _stream_ptr(dev)), "lgx_score_topk")
+    return (idx, val, mm) if want_minmax else (idx, val)
+
+
+def topk_rows(S: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Row-wise top-k of a dense f32 score matrix (tools.h:13-33); ties -> lower column."""
+    require_gpu(S)
+    if S.dtype != torch.float32 or S.dim() != 2 or S.stride(1) != 1:
+        raise TypeError("topk_rows expects a row-major float32 matrix")
+    rows, cols = S.shape
+    idx = torch.empty((rows, k), dtype=torch.int32, device=S.device)
+    val = torch.empty((rows, k), dtype=torch.float32, device=S.device)
+    _lib.check(_lib.lib().lgx_topk_rows(S.data_ptr(), rows, cols, S.stride(0), int(k), idx.data_ptr(), val.data_ptr(),
+                                        _stream_ptr(S.device)), "lgx_topk_rows")
+    return idx, val
+
+
+def inv_log2_table(k: int, device) -> torch.Tensor:
+    """1.0/log2(i+2) with the host libm (as the C++ evaluator computes it, evaluate_foldout.h:80,84)."""
+    return torch.tensor([1.0 / math.log2(i + 2) for i in range(k)], dtype=torch.float64, device=device)
+
+
+def foldout_metrics(rankings: torch.Tensor, truth: Tuple[torch.Tensor, torch.Tensor]) -> torch.Tensor:
+    """evaluate_foldout (evaluate_foldout.h:115-195) -> f32 [users, 5k]."""
+    require_gpu(rankings)
+    r = rankings.to(torch.int32).contiguous()
+    users, k = r.shape
+    out = torch.empty((users, 5 * k), dtype=torch.float32, device=r.device)
+    tl = inv_log2_table(k, r.device)
+    _lib.check(_lib.lib().lgx_foldout_metrics(r.data_ptr(), users, k, truth[0].data_ptr(), truth[1].data_ptr(),
+                                              tl.data_ptr(), out.data_ptr(), _stream_ptr(r.device)),
+               "lgx_foldout_metrics")
+    return out
+
+
+def gather_scores(emb_user: torch.Tensor, emb_item: torch.Tensor, cand: Tuple[torch.Tensor, torch.Tensor],
+                  n_pairs: int) -> torch.Tensor:
+    """Per-user candidate dots (recommend.py:167-171, :214-217) -> f32 [n_pairs]."""
+    require_gpu(emb_user, emb_item)
+    eu = emb_user.to(torch.float32).contiguous()
+    ei = emb_item.to(torch.float32).contiguous()
+    out = torch.empty(max(n_pairs, 1), dtype=torch.float32, device=eu.device)
+    _lib.check(_lib.lib().lgx_gather_scores(eu.data_ptr(), ei.data_ptr(), eu.shape[0], eu.shape[1], cand[0].data_ptr(),
+                                            cand[1].data_ptr(), n_pairs, out.data_ptr(), _stream_ptr(eu.device)),
+               "lgx_gather_scores")
+    return out[:n_pairs]
+
+
+def fill_normal(shape, std: float, seed: int, dtype=torch.float32, device="cuda") -> torch.Tensor:
+    t = torch.empty(shape, dtype=dtype, device=device)
+    require_gpu(t)
+    _lib.check(_lib.lib().lgx_fill_normal(t.data_ptr(), t.numel(), float(std), int(seed) & (2**64 - 1),
+                                          _dtype_code(t), _stream_ptr(t.device)), "lgx_fill_normal")
+    return t

@@ -1,0 +1,196 @@
+/*
+ * lgx.h -- C ABI of liblgx.so, the MI355X (gfx950) LightGCN propagation + scoring engine.
+ *
+ * Conventions
+ *   - extern "C", plain pointers and sizes, no torch / no C++ types.
+ *   - Every data pointer is caller-owned DEVICE memory unless the name ends in `_host`.
+ *     The library never allocates on a compute call: scratch is passed in as `ws` / `ws_bytes`
+ *     sized by the matching *_workspace() query.
+ *   - Every call is stream-ordered on `stream` (a hipStream_t; NULL = the legacy default stream)
+ *     and never synchronises the host, so it can be captured into a hipGraph.
+ *   - Return value: LGX_OK (0) or an LGX_ERR_* code; lgx_last_error() returns a thread-local
+ *     message for the last failing call on this thread.  No C++ exception crosses the ABI.
+ *
+ * Reference interfaces replaced (paths relative to the reference root):
+ *   lgx_build_norm_adj     Loader.getSparseGraph build branch  lightGCN/LightGCN-PyTorch-master/code/dataloader.py:339-376
+ *                          Data.get_adj_mat pre_adj branch      LightGCN-tf/utility/load_data.py:91-104
+ *   lgx_csr_from_coo_rows  _convert_sp_mat_to_sp_tensor + coalesce (dataloader.py:331-337,373-374)
+ *   lgx_propagate_layer /  LightGCN.computer()                  code/model.py:145-177 (torch.sparse.mm :171)
+ *   lgx_propagate          TF _create_lightgcn_embed            LightGCN-tf/LightGCN.py:232-253
+ *   lgx_spmm_csr           torch.sparse.mm(G, X) (forward, and the backward G^T dY = G dY)  model.py:171
+ *   lgx_score_dense        LightGCN.getUsersRating              code/model.py:179-184; TF batch_ratings LightGCN.py:148
+ *   lgx_score_topk         Procedure.Test mask + torch.topk     code/Procedure.py:127-135;
+ *                          batch_test.test mask + evaluator     LightGCN-tf/utility/batch_test.py:47-70
+ *                          recommend.py global min/max          recommend.py:163-164, 375-377
+ *   lgx_topk_rows          c_top_k_array_index                  LightGCN-tf/evaluator/cpp/include/tools.h:13-33
+ *   lgx_foldout_metrics    evaluate_foldout                     LightGCN-tf/evaluator/cpp/include/evaluate_foldout.h:115-195
+ *   lgx_gather_scores      accuracy_cf / elasticity_item per-user candidate dot  recommend.py:167-171, 214-217
+ */
+#ifndef LGX_H
+#define LGX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* lgx_stream_t; /* == hipStream_t */
+
+#define LGX_OK 0
+#define LGX_ERR_INVALID_ARG 1
+#define LGX_ERR_HIP 2
+#define LGX_ERR_UNSUPPORTED 3
+#define LGX_ERR_WORKSPACE 4
+
+#define LGX_DTYPE_F32 0  /* fp32 storage, fp32 arithmetic */
+#define LGX_DTYPE_BF16 1 /* bf16 storage, fp32 accumulate */
+
+/* layer epilogue modes of lgx_propagate_layer (model.py:163-175: embs.append + stack + mean) */
+#define LGX_LAYER_PLAIN 0 /* Y = A X                                                     */
+#define LGX_LAYER_FIRST 1 /* Y = A X ; acc = E0 + Y                                      */
+#define LGX_LAYER_MID 2   /* Y = A X ; acc += Y                                          */
+#define LGX_LAYER_LAST 3  /* out = (acc + A X) / n_mean          (Y not written)         */
+#define LGX_LAYER_ONLY 4  /* out = (E0 + A X) / n_mean           (K == 1, Y not written) */
+
+/*
+ * A row-partitioned CSR operator plus its launch plan.
+ *   indptr [n_rows+1] int64, indices [nnz] int32 (column ids into the X table), vals [nnz] f32.
+ *   The plan cuts every row into segments of at most seg_len nonzeros, ordered by length
+ *   (longest first); a row with more than one segment is a "split" row whose segments write fp32
+ *   partial sums to partials[slot] and are reduced, in slot order (deterministic), by a fix-up
+ *   pass.  Built host-side by factors_of_serendipity_recommendation_amd.graph.make_plan().
+ *     seg_row  [n_segs]  int32   row of the segment
+ *     seg_part [n_segs]  int32   segment index inside its row (0 for unsplit rows)
+ *     seg_slot [n_segs]  int32   partial slot, or -1 for an unsplit row
+ *     split_row[n_split] int32   split rows
+ *     split_ptr[n_split+1] int32 slot range of each split row
+ *     partials [n_partials * d] f32 scratch (may be NULL when n_split == 0)
+ */
+typedef struct lgx_csr {
+    const int64_t* indptr;
+    const int32_t* indices;
+    const float* vals;
+    int64_t n_rows;
+    int64_t n_cols;
+    int64_t nnz;
+    const int32_t* seg_row;
+    const int32_t* seg_part;
+    const int32_t* seg_slot;
+    int64_t n_segs;
+    int64_t seg_len;
+    const int32_t* split_row;
+    const int32_t* split_ptr;
+    int64_t n_split;
+    int64_t n_partials;
+    float* partials;
+} lgx_csr;
+
+const char* lgx_version(void);
+const char* lgx_last_error(void);
+/* arch_out receives e.g. "gfx950:sramecc+:xnack-"; cu/xcd counts from hipDeviceProp_t. */
+int lgx_device_info(int device, int* cu_count, int* xcd_count, char* arch_out, size_t arch_len);
+
+/* ---------------------------------------------------------------- a2: graph build */
+/* Workspace bytes for lgx_build_norm_adj. */
+int lgx_build_norm_adj_workspace(int64_t n_edges, int64_t n_users, int64_t n_items, size_t* ws_bytes);
+/*
+ * D^-1/2 [[0,R],[R^T,0]] D^-1/2 as CSR over N = n_users + n_items rows, columns sorted.
+ * dedup = 0: duplicate (u,i) pairs are summed (PyTorch Loader, dataloader.py:288);
+ * dedup = 1: duplicates collapse to 1 (TF Data dok matrix, load_data.py:61).
+ * indices / vals must hold 2*n_edges entries; the true nnz is indptr[N] (device) -- read it back
+ * when needed.  d_r = (float)(1/sqrt((double)deg_r)) (0 for isolated rows), val = (d_r*a)*d_c:
+ * bit-exact with the reference's s_pre_adj_mat.npz.
+ */
+int lgx_build_norm_adj(const int32_t* user_idx, const int32_t* item_idx, int64_t n_edges,
+                       int64_t n_users, int64_t n_items, int dedup, int64_t* indptr,
+                       int32_t* indices, float* vals, void* ws, size_t ws_bytes,
+                       lgx_stream_t stream);
+/* indptr [n_rows+1] from the row ids of a row-sorted (coalesced) COO matrix. */
+int lgx_csr_from_coo_rows(const int64_t* coo_rows, int64_t nnz, int64_t n_rows, int64_t* indptr,
+                          lgx_stream_t stream);
+
+/* ---------------------------------------------------------------- a4/a5: propagation */
+/*
+ * One LightGCN layer over the rows of A (row r = local output row r).
+ *   X  [n_cols, d]  dtype     input table (columns of A index its rows)
+ *   Y  [n_rows, d]  dtype     next-layer table (PLAIN / FIRST / MID)
+ *   E0 [n_rows, d]  dtype     layer-0 rows (FIRST / ONLY)
+ *   acc[n_rows, d]  f32       running layer sum (FIRST / MID / LAST)
+ *   out[n_rows, d]  f32       layer mean (LAST / ONLY), divided by n_mean (= K+1)
+ * d: multiple of 4 (f32) or 8 (bf16), <= 1024.
+ */
+int lgx_propagate_layer(const lgx_csr* A, const void* X, void* Y, const void* E0, float* acc,
+                        float* out, int64_t d, int dtype, int mode, float n_mean,
+                        lgx_stream_t stream);
+/* Y = A X (alias of lgx_propagate_layer with LGX_LAYER_PLAIN). */
+int lgx_spmm_csr(const lgx_csr* A, const void* X, void* Y, int64_t d, int dtype, lgx_stream_t stream);
+/* Workspace bytes of lgx_propagate: 2 x [N,d] dtype ping-pong tables + [N,d] f32 layer sum. */
+int lgx_propagate_workspace(int64_t n_rows, int64_t d, int dtype, size_t* ws_bytes);
+/* Whole K-layer propagation (square A, X = E0 table [N,d] dtype) -> out [N,d] f32 layer mean. */
+int lgx_propagate(const lgx_csr* A, const void* E0, float* out, int64_t d, int K, int dtype,
+                  void* ws, size_t ws_bytes, lgx_stream_t stream);
+
+/* ---------------------------------------------------------------- a6-a9: scoring / top-k */
+/*
+ * scores[b, i] = <Q[user_rows ? user_rows[b] : b], items[i]>  (optionally sigmoid), f32 [B, n_items].
+ */
+int lgx_score_dense(const void* Q, const int64_t* user_rows, const void* items, int64_t B,
+                    int64_t n_items, int64_t d, int dtype, int apply_sigmoid, float* scores,
+                    lgx_stream_t stream);
+/* Workspace bytes of lgx_score_topk for this shape (item-split partial lists). */
+int lgx_score_topk_workspace(int64_t B, int64_t n_items, int k, size_t* ws_bytes);
+/*
+ * Fused full-catalog scoring + positive mask + top-k; [B, n_items] is never materialised.
+ *   mask_indptr [B+1] int64 / mask_indices int32 sorted per row: items excluded for query b
+ *   (may be NULL).  Masked items rank after every unmasked item with value mask_value.
+ *   Ranking: higher raw score first, ties -> lower item id.  out_val = raw score, or
+ *   sigmoid(score) if apply_sigmoid.  minmax_out (NULL = skip) receives {min, max} of ALL raw
+ *   scores (before masking) as f32[2].  k in [1, 64].
+ */
+int lgx_score_topk(const void* Q, const int64_t* user_rows, const void* items, int64_t B,
+                   int64_t n_items, int64_t d, int dtype, const int64_t* mask_indptr,
+                   const int32_t* mask_indices, int k, float mask_value, int apply_sigmoid,
+                   int32_t* out_idx, float* out_val, float* minmax_out, void* ws,
+                   size_t ws_bytes, lgx_stream_t stream);
+/* Row-wise top-k of a dense f32 matrix (row stride ld), ties -> lower column.  k in [1, 64]. */
+int lgx_topk_rows(const float* S, int64_t rows, int64_t cols, int64_t ld, int k, int32_t* out_idx,
+                  float* out_val, lgx_stream_t stream);
+
+/* ---------------------------------------------------------------- a10: metric curves */
+/*
+ * evaluate_foldout: rankings [users, k] int32 + ragged truths (truth_indptr [users+1] int64,
+ * truth_indices int32) -> results [users, 5k] f32 = [precision | recall | ap | ndcg | mrr].
+ * inv_log2 [k] f64 = 1/log2(i+2) (host libm values, copied to device by the caller).
+ */
+int lgx_foldout_metrics(const int32_t* rankings, int64_t users, int k, const int64_t* truth_indptr,
+                        const int32_t* truth_indices, const double* inv_log2, float* results,
+                        lgx_stream_t stream);
+
+/* ---------------------------------------------------------------- a11/a12: candidate similarity */
+/*
+ * scores[p] = <emb_user[row of p], emb_item[cand_items[p]]> for the ragged candidate lists
+ * cand_indptr [U+1] int64 / cand_items int32 (f32 tables); n_pairs = cand_indptr[U] (host value).
+ */
+int lgx_gather_scores(const float* emb_user, const float* emb_item, int64_t n_users, int64_t d,
+                      const int64_t* cand_indptr, const int32_t* cand_items, int64_t n_pairs,
+                      float* scores, lgx_stream_t stream);
+
+/* ---------------------------------------------------------------- synthetic graphs (bench) */
+/*
+ * Deterministic synthetic bipartite edges: user u owns edges [user_offsets[u], user_offsets[u+1]);
+ * each edge draws an item by inverse-CDF sampling of item_cdf [n_items] (non-decreasing, last = 1)
+ * from a counter-based hash of (seed, edge id), then maps it through item_perm [n_items] (NULL =
+ * identity).  n_edges = user_offsets[n_users] (host value).  Same output on every device / rank.
+ */
+int lgx_synth_edges(uint64_t seed, const int64_t* user_offsets, int64_t n_users,
+                    const float* item_cdf, const int32_t* item_perm, int64_t n_items,
+                    int64_t n_edges, int32_t* users_out, int32_t* items_out, lgx_stream_t stream);
+/* Deterministic N(0, std^2) fill (Box-Muller over a counter hash), dtype f32 or bf16. */
+int lgx_fill_normal(void* out, int64_t n, float std, uint64_t seed, int dtype, lgx_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LGX_H */

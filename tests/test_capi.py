@@ -1,0 +1,58 @@
+"""CPU: liblgx.so loads and exports every entry point declared in include/lgx.h; argument checks
+fail loudly without touching the GPU."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    src = open(os.path.join(ROOT, "include", "lgx.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(lgx_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    names = declared_functions()
+    for n in ["lgx_build_norm_adj", "lgx_propagate", "lgx_propagate_layer", "lgx_spmm_csr", "lgx_score_topk",
+              "lgx_score_dense", "lgx_topk_rows", "lgx_foldout_metrics", "lgx_gather_scores", "lgx_version"]:
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol():
+    from factors_of_serendipity_recommendation_amd import _lib
+    L = _lib.lib()
+    for name in declared_functions():
+        assert hasattr(L, name), name
+        assert name in _lib.SIGNATURES, f"{name} has no ctypes signature"
+
+
+def test_version_and_error_channel():
+    from factors_of_serendipity_recommendation_amd import _lib
+    L = _lib.lib()
+    assert b"gfx950" in L.lgx_version()
+    # k outside [1, 64] is rejected before any device work
+    rc = L.lgx_topk_rows(None, 1, 10, 10, 0, None, None, None)
+    assert rc != 0
+    rc = L.lgx_topk_rows(ctypes.c_void_p(16), 1, 10, 10, 65, ctypes.c_void_p(16), None, None)
+    assert rc == 3 and b"k=65" in L.lgx_last_error()
+    with pytest.raises(RuntimeError, match="lgx_topk_rows"):
+        _lib.check(rc, "lgx_topk_rows")
+
+
+def test_lgx_csr_struct_layout_matches_header():
+    from factors_of_serendipity_recommendation_amd import _lib
+    # 16 fields: 9 pointers + 7 int64 -> 128 bytes on LP64
+    assert ctypes.sizeof(_lib.LgxCSR) == 16 * 8
+
+
+def test_ops_refuse_cpu_tensors():
+    import torch
+    import factors_of_serendipity_recommendation_amd as lgx
+    with pytest.raises(RuntimeError, match="GPU only"):
+        lgx.topk_rows(torch.zeros(2, 4), 1)
+    with pytest.raises(RuntimeError, match="GPU only"):
+        lgx.score_topk(torch.zeros(2, 8), torch.zeros(3, 8), 1)

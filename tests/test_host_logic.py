@@ -1,0 +1,117 @@
+"""CPU: host-side logic of the package -- launch plans, shard partitioning and column remapping,
+ragged-list packing, the synthetic degree law and the Loader's file parsing."""
+import numpy as np
+import pytest
+import torch
+
+from factors_of_serendipity_recommendation_amd.distributed import balanced_bounds, make_shard, pad_table
+from factors_of_serendipity_recommendation_amd.graph import CSRGraph, choose_seg_len, make_plan
+from factors_of_serendipity_recommendation_amd.ops import lists_to_device_csr
+from factors_of_serendipity_recommendation_amd.synth import user_degrees
+from oracle import oracle
+
+
+def _check_plan(indptr, plan):
+    lens = np.diff(indptr)
+    seen = np.zeros(int(indptr[-1]), dtype=np.int64)
+    rows_seen = np.zeros(len(lens), dtype=np.int64)
+    for r, part, slot in zip(plan.seg_row, plan.seg_part, plan.seg_slot):
+        b = indptr[r] + part * plan.seg_len
+        e = indptr[r + 1] if slot < 0 else min(indptr[r + 1], b + plan.seg_len)
+        seen[b:e] += 1
+        rows_seen[r] += 1
+        if slot >= 0:
+            assert lens[r] > plan.seg_len
+    assert np.all(seen == 1), "every nonzero covered exactly once"
+    assert np.all(rows_seen >= 1), "every row (even empty) has a segment"
+    # split rows own contiguous slot ranges in part order
+    for j, r in enumerate(plan.split_row):
+        slots = plan.seg_slot[plan.seg_row == r]
+        parts = plan.seg_part[plan.seg_row == r]
+        assert np.array_equal(np.sort(slots), np.arange(plan.split_ptr[j], plan.split_ptr[j + 1]))
+        assert np.array_equal(slots - plan.split_ptr[j], parts)
+
+
+@pytest.mark.parametrize("seg_len", [1, 2, 7, 64, 1000])
+def test_make_plan_covers_every_nonzero_once(seg_len):
+    rng = np.random.default_rng(seg_len)
+    lens = rng.zipf(1.5, 400) % 3000
+    lens[::17] = 0
+    indptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    plan = make_plan(indptr, seg_len)
+    _check_plan(indptr, plan)
+    # longest-first order
+    seg_lens = np.minimum(lens[plan.seg_row] - plan.seg_part * seg_len, seg_len)
+    seg_lens = np.where(plan.seg_slot < 0, lens[plan.seg_row], seg_lens)
+    assert np.all(np.diff(lens[plan.seg_row]) <= 0)
+
+
+def test_choose_seg_len_range():
+    assert choose_seg_len(0) == 64
+    assert choose_seg_len(2_000_000) == 64
+    assert choose_seg_len(1_000_000_000) == 2048
+
+
+def test_balanced_bounds():
+    lens = np.array([5, 0, 0, 100, 1, 1, 1, 50, 3, 3])
+    indptr = np.concatenate([[0], np.cumsum(lens)])
+    for world in (1, 2, 3, 4, 8):
+        b = balanced_bounds(indptr, 0, len(lens), world)
+        assert b[0] == 0 and b[-1] == len(lens) and np.all(np.diff(b) >= 0) and len(b) == world + 1
+
+
+def _cpu_graph(U, I, E, seed):
+    rng = np.random.default_rng(seed)
+    u = rng.integers(0, U, E).astype(np.int32)
+    i = rng.integers(0, I, E).astype(np.int32)
+    ip, ix, iv = oracle.build_norm_adj(u, i, U, I)
+    return CSRGraph(torch.from_numpy(ip), torch.from_numpy(ix), torch.from_numpy(iv), U + I, U + I, U, I), (ip, ix, iv)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_make_shard_remaps_columns_into_padded_tables(world):
+    U, I = 70, 50
+    A, (ip, ix, iv) = _cpu_graph(U, I, 900, world)
+    X = torch.from_numpy(np.random.default_rng(0).standard_normal((U + I, 4)).astype(np.float32))
+    full = oracle.spmm(ip, ix, iv, X.numpy())
+    for rank in range(world):
+        s = make_shard(A, U, I, rank, world, seg_len=8)
+        Xi = pad_table(X[U:], s.item_bounds, s.mi)
+        Xu = pad_table(X[:U], s.user_bounds, s.mu)
+        yu = oracle.spmm(s.A_ui.indptr.numpy(), s.A_ui.indices.numpy(), s.A_ui.vals.numpy(), Xi.numpy())
+        yi = oracle.spmm(s.A_iu.indptr.numpy(), s.A_iu.indices.numpy(), s.A_iu.vals.numpy(), Xu.numpy())
+        u0, u1 = s.user_bounds[rank], s.user_bounds[rank + 1]
+        i0, i1 = s.item_bounds[rank], s.item_bounds[rank + 1]
+        assert np.allclose(yu, full[u0:u1])
+        assert np.allclose(yi, full[U + i0:U + i1])
+
+
+def test_lists_to_csr_packing():
+    ip, ix = lists_to_device_csr([[5, 1], [], [3]], "cpu")
+    assert ip.tolist() == [0, 2, 2, 3] and ix.tolist() == [1, 5, 3]
+    ip, ix = lists_to_device_csr([[5, 1]], "cpu", sort=False)
+    assert ix.tolist() == [5, 1]
+
+
+def test_user_degrees_law():
+    deg = user_degrees(10000, 500, 200000, 1.0, 0)
+    assert deg.min() >= 1 and deg.max() <= 250
+    assert abs(int(deg.sum()) - 200000) / 200000 < 0.2
+
+
+def test_loader_parses_reference_format(tmp_path, mlls):
+    from factors_of_serendipity_recommendation_amd.dataloader import Loader
+    tp, tx = mlls["train_list_indptr"], mlls["train_list_indices"]
+    with open(tmp_path / "train.txt", "w") as f:
+        for j, u in enumerate(mlls["train_list_users"]):
+            f.write(" ".join(str(x) for x in [u] + list(tx[tp[j]:tp[j + 1]])) + "\n")
+    sp_, sx = mlls["test_indptr"], mlls["test_indices"]
+    with open(tmp_path / "test.txt", "w") as f:
+        for j, u in enumerate(mlls["test_users"]):
+            f.write(" ".join(str(x) for x in [u] + list(sx[sp_[j]:sp_[j + 1]])) + "\n")
+    ds = Loader(path=str(tmp_path), device="cpu", cache_adj=False)
+    assert ds.n_users == int(mlls["n_users"]) and ds.m_items == int(mlls["n_items"])
+    assert ds.trainDataSize == len(mlls["train_items"])
+    u0 = int(mlls["test_users"][0])
+    assert sorted(ds.testDict[u0]) == sorted(sx[sp_[0]:sp_[1]].tolist())
+    assert np.array_equal(np.sort(ds.allPos[0]), np.sort(tx[tp[0]:tp[1]]))
