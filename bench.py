@@ -61,6 +61,24 @@ def max_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
+def measured_traffic(config: str, world: int, kernels) -> tuple:
+    """HBM bytes per launch from the newest committed rocprofv3 PMC summary for this workload
+    (profiles/rNN_<config>_pmc_traffic.json; (2*FETCH_SIZE + WRITE_SIZE) per MI355X_MICROARCH.md).
+    Returns (GB per launch or None, source file)."""
+    import glob
+    if world != 1:
+        return None, None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_pmc_traffic.json")))
+    if not files:
+        return None, None
+    doc = json.load(open(files[-1]))
+    try:
+        b = sum(doc["kernels"][k]["hbm_bytes_per_launch"] for k in kernels)
+    except KeyError:
+        return None, None
+    return b / 1e9, os.path.relpath(files[-1], ROOT)
+
+
 def layer_bytes(nnz: int, rows: int, d: int, s: int) -> int:
     return nnz * (4 + 4 + d * s) + rows * d * s + 8 * (rows + 1)
 
@@ -142,11 +160,13 @@ def bench_propagation(args, rank, world):
     bytes_per_launch = float(np.mean([b for _, _, b in timings]))
     achieved = bytes_per_launch / mean_launch_s
     edges = K * nnz_all * args.steps
+    traffic, traffic_src = measured_traffic(cfg.name, world, ["spmm_segments", "spmm_fixup"])
     res = {
         "cfg": cfg, "dtype": "bf16" if es == 2 else "f32", "value": edges / elapsed,
         "ms_per_step": elapsed / args.steps * 1e3, "nnz": nnz_all,
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK, "traffic": None,
+                     "frac": achieved / HBM_PEAK, "traffic": traffic, "traffic_unit": "GB/launch",
+                     "traffic_source": traffic_src,
                      "kernel": "spmm_segments (+spmm_fixup)", "bytes_per_launch": int(bytes_per_launch),
                      "mean_launch_ms": mean_launch_s * 1e3},
         "graph": A if world == 1 else None, "E0": E0 if world == 1 else None,
@@ -202,10 +222,12 @@ def bench_scoring(args, rank, world):
     elapsed = max_over_ranks(time.perf_counter() - t_start, world)
     mean_launch = float(np.mean([a.elapsed_time(b) for a, b in ev])) / 1e3
     flops = 2.0 * B * n_items * d
+    traffic, traffic_src = measured_traffic(args.config, world, ["score_topk_kernel"])
     return {"value": B_total * n_items * steps / elapsed, "unit": "items/s", "users_per_step": B_total,
             "n_items": n_items, "d": d, "k": k, "dtype": "bf16", "ms_per_step": elapsed / steps * 1e3,
             "roofline": {"bound": "mfma", "achieved": flops / mean_launch / 1e12, "peak": BF16_MFMA_PEAK / 1e12,
-                         "unit": "TFLOP/s", "frac": flops / mean_launch / BF16_MFMA_PEAK, "traffic": None,
+                         "unit": "TFLOP/s", "frac": flops / mean_launch / BF16_MFMA_PEAK, "traffic": traffic,
+                         "traffic_unit": "GB/launch", "traffic_source": traffic_src,
                          "kernel": "score_topk_kernel (+finalize)"}}
 
 
