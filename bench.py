@@ -238,12 +238,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="synth10m", choices=sorted(CONFIGS))
     ap.add_argument("--dtype", default=None, choices=[None, "bf16", "f32"])
-    ap.add_argument("--score-users", type=int, default=32768)
+    ap.add_argument("--score-users", type=int, default=1_000_000)
     ap.add_argument("--score-items", type=int, default=1_000_000)
-    ap.add_argument("--score-steps", type=int, default=3)
+    ap.add_argument("--score-steps", type=int, default=2)
     ap.add_argument("--cpu-nnz", type=int, default=6_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scoring", action="store_true")
+    ap.add_argument("--no-propagation", action="store_true", help="development: scoring leg only")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -255,6 +256,11 @@ def main():
     if world != args.gpus:
         log(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}")
 
+    if args.no_propagation:
+        sc = bench_scoring(args, rank, world)
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "scoring": sc}), flush=True)
+        return
     res = bench_propagation(args, rank, world)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
