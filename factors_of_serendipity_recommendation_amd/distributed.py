@@ -11,8 +11,10 @@ user row only references item columns and vice versa, so each rank holds two loc
     A_ui : local user rows -> item columns,  A_iu : local item rows -> user columns
 with their column ids rewritten once into PADDED coordinates: rank q's item block lives at rows
 [q*mi, q*mi + n_q) of an item table of world*mi rows (mi = max block size), likewise for users.
-A layer's local output slab is then exactly the all_gather_into_tensor input of that rank, and
-the gathered table needs no reshuffle.
+A layer's local output is written to a [mi, d] send buffer which is exactly this rank's
+all_gather_into_tensor input, and the gathered table needs no reshuffle.  Send buffers ping-pong
+by layer parity (the gather of layer k may still be reading one while layer k+1 of the same side
+is computed into the other).
 
 Overlap.  Layer k+1 of the users needs layer k of the items and vice versa, so the K layers form
 two independent chains (I0 -> U1 -> I2 -> U3 ... and U0 -> I1 -> U2 -> I3 ...).  Steps are issued
@@ -143,6 +145,8 @@ class ShardedPropagation:
                   [torch.zeros((s.world * s.mu, d), dtype=dt, device=dev) for _ in range(2)]
         self.Xi = [pad_table(E0_item, s.item_bounds, s.mi)] + \
                   [torch.zeros((s.world * s.mi, d), dtype=dt, device=dev) for _ in range(2)]
+        self.send_u = [torch.zeros((s.mu, d), dtype=dt, device=dev) for _ in range(2)]
+        self.send_i = [torch.zeros((s.mi, d), dtype=dt, device=dev) for _ in range(2)]
         self.acc_u = torch.zeros((s.n_u_local, d), dtype=torch.float32, device=dev)
         self.acc_i = torch.zeros((s.n_i_local, d), dtype=torch.float32, device=dev)
         self.out_u = torch.zeros((s.n_u_local, d), dtype=torch.float32, device=dev)
@@ -165,12 +169,11 @@ class ShardedPropagation:
         r = self.s.rank
         return table[r * pad:r * pad + n_local]
 
-    def _gather(self, table: torch.Tensor, pad: int):
-        if self.s.world == 1:
+    def _gather(self, table: torch.Tensor, send: torch.Tensor, n_local: int):
+        if self.s.world == 1:  # the single "gather" is a copy into the table
+            table[:n_local].copy_(send[:n_local])  # (plumbing: a device memcpy)
             return None
-        r = self.s.rank
-        src = table[r * pad:(r + 1) * pad]
-        return dist.all_gather_into_tensor(table, src, group=self.group, async_op=True)
+        return dist.all_gather_into_tensor(table, send, group=self.group, async_op=True)
 
     def schedule(self) -> List[Tuple[str, int]]:
         """Issue order: alternate the two chains (U1, I1, I2, U2, U3, I3, ...)."""
@@ -192,18 +195,18 @@ class ShardedPropagation:
             mode = self._mode(k)
             if side == "u":
                 A, X = s.A_ui, self.Xi[self._buf(k - 1)]
-                Yt, pad, n_loc = self.Xu[self._buf(k)], s.mu, s.n_u_local
+                Yt, send, n_loc = self.Xu[self._buf(k)], self.send_u[k & 1], s.n_u_local
                 E0 = self._slab(self.Xu[0], s.mu, n_loc)
                 acc, out = self.acc_u, self.out_u
             else:
                 A, X = s.A_iu, self.Xu[self._buf(k - 1)]
-                Yt, pad, n_loc = self.Xi[self._buf(k)], s.mi, s.n_i_local
+                Yt, send, n_loc = self.Xi[self._buf(k)], self.send_i[k & 1], s.n_i_local
                 E0 = self._slab(self.Xi[0], s.mi, n_loc)
                 acc, out = self.acc_i, self.out_i
-            Y = self._slab(Yt, pad, n_loc) if k < self.K else None
+            Y = send[:n_loc] if k < self.K else None
             self.layer_fn(A, X, mode, Y=Y, E0=E0, acc=acc, out=out, n_mean=float(self.K + 1))
             if k < self.K:
-                pending[(side, k)] = self._gather(Yt, pad)
+                pending[(side, k)] = self._gather(Yt, send, n_loc)
         for h in pending.values():
             if h is not None:
                 h.wait()

@@ -1,0 +1,75 @@
+"""GPU: the multi-GPU propagation schedule with the REAL HIP layer kernels.  The box has one GPU,
+so the two ranks share cuda:0 and exchange over gloo (RCCL refuses two ranks on one device); the
+8-GPU RCCL run is the bench's job.  Checked against the float64 oracle (fp32 tolerance)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, K, dtype_name, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle
+        import factors_of_serendipity_recommendation_amd as lgx
+        from factors_of_serendipity_recommendation_amd.distributed import ShardedPropagation, make_shard
+        dtype = torch.float32 if dtype_name == "f32" else torch.bfloat16
+        rng = np.random.default_rng(5)
+        U, I, E = 3000, 2000, 60000
+        u = rng.integers(0, U, E).astype(np.int32)
+        i = (rng.zipf(1.3, E) % I).astype(np.int32)
+        A = lgx.build_norm_adj(u, i, U, I, dedup=True, device="cuda:0")
+        E0 = (torch.from_numpy(rng.standard_normal((U + I, 64)).astype(np.float32)) * 0.1)
+        if dtype == torch.bfloat16:
+            E0 = E0.to(torch.bfloat16).float()
+        shard = make_shard(A, U, I, rank, world, seg_len=64)
+        prop = ShardedPropagation(shard, E0[:U].cuda().to(dtype), E0[U:].cuda().to(dtype), K)
+        prop.step()
+        prop.step()
+        ou, oi = prop.gather_outputs()
+        torch.cuda.synchronize()
+        if rank == 0:
+            ref = oracle.propagate(A.indptr.cpu().numpy(), A.indices.cpu().numpy(), A.vals.cpu().numpy(),
+                                   E0.numpy(), K)
+            got = np.concatenate([ou.cpu().numpy(), oi.cpu().numpy()])
+            err = np.abs(got - ref)
+            rel = 1e-5 if dtype == torch.float32 else 2e-2
+            tol = rel * np.abs(ref) + rel * np.sqrt(np.mean(ref ** 2))
+            q.put((bool((err <= tol).all()), float(err.max())))
+    except Exception as e:  # surface the failure to the parent
+        if rank == 0:
+            q.put((False, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,K,dt", [(2, 3, "f32"), (2, 4, "bf16"), (3, 2, "f32")])
+def test_sharded_propagation_real_kernels(world, K, dt):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, K, dt, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    ok, info = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+    assert ok, info
+    assert all(p.exitcode == 0 for p in procs)

@@ -408,3 +408,33 @@ def test_eigenvector_property_full_size_10m():
     A = synth_graph(cfg, 2020, DEV)
     assert A.nnz == 2 * cfg.n_edges
     _eigen_check(A, torch.bfloat16, cfg.K)
+
+
+# ------------------------------------------------------------------------------------ recommend.py
+def test_accuracy_cf_dropin(tmp_path):
+    from factors_of_serendipity_recommendation_amd import recommend
+    rng = np.random.default_rng(12)
+    U, I, d = 150, 4000, 64
+    eu = rng.standard_normal((U, d)).astype(np.float32)
+    ei = rng.standard_normal((I, d)).astype(np.float32)
+    ds = tmp_path / "data" / "toy"
+    ds.mkdir(parents=True)
+    np.save(ds / "emb_user.npy", eu)
+    np.save(ds / "emb_item.npy", ei)
+    mat_candidate = {u: list(rng.choice(I, 1000 - (u % 7), replace=False)) for u in range(U)}
+    recommend.accuracy_cf(mat_candidate, "toy", 3, K=20, data_root=str(tmp_path / "data"))
+    got = np.load(ds / "rec" / "3" / "rec_acc.npy")
+    ref = oracle.accuracy_cf(eu, ei, mat_candidate, 20)
+    assert got.shape == (U, 20)
+    for u in range(U):  # argpartition semantics: compare the top-K SETS
+        assert set(got[u].tolist()) == set(ref[u].tolist())
+
+
+def test_similarity_minmax():
+    from factors_of_serendipity_recommendation_amd import recommend
+    rng = np.random.default_rng(13)
+    eu = rng.standard_normal((333, 64)).astype(np.float32)
+    ei = rng.standard_normal((2500, 64)).astype(np.float32)
+    mn, mx = recommend.similarity_minmax(torch.from_numpy(eu).to(DEV), torch.from_numpy(ei).to(DEV))
+    omn, omx = oracle.similarity_minmax(eu, ei)
+    assert abs(mn - omn) <= 1e-5 * abs(omn) and abs(mx - omx) <= 1e-5 * abs(omx)
