@@ -108,11 +108,20 @@ __device__ __forceinline__ bool is_masked(const ScoreArgs& a, int64_t b, int32_t
 // output row (item offset inside the 32-item tile) of accumulator register r for lane half h
 __device__ __forceinline__ int tile_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// LDS bytes of the per-wave lists: keys [32][kstride] u64 + meta [32][2] i32 (16-B aligned rows,
+// plus one spare row so the vectorised rescan of the last user stays inside the allocation)
+__host__ __device__ constexpr int kstride(int k) { return (k + 1) & ~1; }
+constexpr int kListSpare = 8;  // the 8-key rescan of user 31 may read past its row
+__host__ __device__ constexpr size_t list_bytes_per_wave(int k) {
+    return ((size_t)kUsersPerWave * kstride(k) + kListSpare) * 8 + kUsersPerWave * 8;
+}
+
 // Running top-k of the 32 users of one wave (lanes col and col+32 share user col).  User col's
 // list is an UNSORTED array of k packed keys in LDS (wave_topk.h key order) plus {len, argmin};
 // the lane mirrors the worst kept entry (tau, tau_i) in registers for the per-score filter.  An
 // accepted candidate overwrites the worst entry and the new worst is found by one scan of k
 // independent LDS reads -- no dependent shift chain.  Lists are sorted only when merged.
+template <int KMAX>
 struct WaveTopK {
     uint64_t* keys;  // this lane's user: [k]
     int32_t* meta;   // this lane's user: {len, argmin}
@@ -123,6 +132,43 @@ struct WaveTopK {
     int32_t tau_i;
     bool full;
     float mn, mx;
+    // 256-bit Bloom filter of the user's masked items (2 hashes), as 8 scalars so that the
+    // word select stays in registers
+    uint32_t bl0, bl1, bl2, bl3, bl4, bl5, bl6, bl7;
+
+    __device__ __forceinline__ static uint32_t bloom_h1(int32_t x) { return ((uint32_t)x * 0x9E3779B1u) >> 24; }
+    __device__ __forceinline__ static uint32_t bloom_h2(int32_t x) { return ((uint32_t)x * 0x85EBCA77u) >> 24; }
+    __device__ __forceinline__ bool bloom_test(uint32_t hv) const {
+        // AND with per-word masks: no select over loaded members (which the compiler would turn
+        // into a load through a selected pointer and force the state into scratch)
+        const uint32_t q = hv >> 5, m = 1u << (hv & 31);
+        const uint32_t hit = (bl0 & (q == 0 ? m : 0u)) | (bl1 & (q == 1 ? m : 0u)) |
+                             (bl2 & (q == 2 ? m : 0u)) | (bl3 & (q == 3 ? m : 0u)) |
+                             (bl4 & (q == 4 ? m : 0u)) | (bl5 & (q == 5 ? m : 0u)) |
+                             (bl6 & (q == 6 ? m : 0u)) | (bl7 & (q == 7 ? m : 0u));
+        return hit != 0u;
+    }
+    __device__ __forceinline__ void bloom_set(uint32_t hv) {
+        const uint32_t q = hv >> 5, m = 1u << (hv & 31);
+        bl0 |= q == 0 ? m : 0u; bl1 |= q == 1 ? m : 0u; bl2 |= q == 2 ? m : 0u; bl3 |= q == 3 ? m : 0u;
+        bl4 |= q == 4 ? m : 0u; bl5 |= q == 5 ? m : 0u; bl6 |= q == 6 ? m : 0u; bl7 |= q == 7 ? m : 0u;
+    }
+    // exact test only when the filter cannot rule the item out
+    __device__ __forceinline__ bool masked(const ScoreArgs& a, int32_t it) const {
+        if (!a.mask_indptr) return false;
+        if (!bloom_test(bloom_h1(it)) || !bloom_test(bloom_h2(it))) return false;
+        return is_masked(a, b, it);
+    }
+    __device__ __forceinline__ void build_bloom(const ScoreArgs& a) {
+        bl0 = bl1 = bl2 = bl3 = bl4 = bl5 = bl6 = bl7 = 0u;
+        if (!a.mask_indptr || !user_ok) return;
+        const int64_t m0 = a.mask_indptr[b], m1 = a.mask_indptr[b + 1];
+        for (int64_t j = m0; j < m1; ++j) {
+            const int32_t x = a.mask_indices[j];
+            bloom_set(bloom_h1(x));
+            bloom_set(bloom_h2(x));
+        }
+    }
 
     __device__ __forceinline__ void init(uint64_t* keys_w, int32_t* meta_w, int k_, int lane, int64_t b_, bool ok) {
         k = k_;
@@ -130,7 +176,7 @@ struct WaveTopK {
         h = lane >> 5;
         b = b_;
         user_ok = ok;
-        keys = keys_w + col * k;
+        keys = keys_w + col * kstride(k);
         meta = meta_w + col * 2;
         if (h == 0) {
             meta[0] = 0;
@@ -145,14 +191,25 @@ struct WaveTopK {
         mx = -INFINITY;
     }
 
+    // new worst entry: 8 keys (four 16-byte reads issued together) per LDS round trip
     __device__ __forceinline__ void rescan() {
-        uint64_t m = keys[0];
+        uint64_t m = ~0ull;
         int mp = 0;
-        for (int j = 1; j < k; ++j) {
-            const uint64_t v = keys[j];
-            if (v < m) {
-                m = v;
-                mp = j;
+        for (int j0 = 0; j0 < k; j0 += 8) {
+            uint64_t v[8];
+#pragma unroll
+            for (int j = 0; j < 8; j += 2) {
+                const ulonglong2 p = *reinterpret_cast<const ulonglong2*>(keys + j0 + j);
+                v[j] = p.x;
+                v[j + 1] = p.y;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint64_t x = (j0 + j < k) ? v[j] : ~0ull;
+                if (x < m) {
+                    m = x;
+                    mp = j0 + j;
+                }
             }
         }
         meta[1] = mp;
@@ -162,7 +219,7 @@ struct WaveTopK {
     // Fast path: ONE compare per score against tau (-inf until the list is full, +inf for padding
     // users), OR-ed into a wave-wide flag; only a tile with a survivor re-tests exactly (bounds,
     // index tie-break) and inserts.  FULL: the whole 32-item tile is inside [i0, i_end).
-    template <bool MINMAX, bool FULL>
+    template <bool MINMAX, bool FULL, bool FASTONLY = false>
     __device__ __forceinline__ void tile(const ScoreArgs& a, const f32x16& acc, int64_t i0, int64_t i_end) {
         bool any = false;
 #pragma unroll
@@ -174,6 +231,10 @@ struct WaveTopK {
                 mx = fmaxf(mx, s);
             }
             any |= in && s >= tau;
+        }
+        if (FASTONLY) {  // development ablation: filter only
+            mn = fminf(mn, __ballot(any) ? 1.0f : 0.0f);
+            return;
         }
         if (__ballot(any) == 0ull) return;  // wave-uniform fast path
         uint32_t cmask = 0;
@@ -187,18 +248,22 @@ struct WaveTopK {
             if (__ballot(ph == h && cmask != 0) == 0ull) continue;
             if (ph == h && cmask) {
                 int len = meta[0];
+                uint32_t todo = cmask;
+                while (todo) {  // one copy of the insertion code, one iteration per survivor
+                    const int r = __builtin_ctz(todo);
+                    todo &= todo - 1;
+                    float sc = acc[0];
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    if (!((cmask >> r) & 1u)) continue;
+                    for (int q = 1; q < 16; ++q) sc = (r == q) ? acc[q] : sc;
                     const int32_t it = (int32_t)(i0 + tile_row(r, h));
-                    const uint64_t key = make_key(acc[r], it);
+                    const uint64_t key = make_key(sc, it);
                     if (len == k) {
                         const int mp = meta[1];
-                        if (key <= keys[mp] || is_masked(a, b, it)) continue;
+                        if (key <= keys[mp] || masked(a, it)) continue;
                         keys[mp] = key;
                         rescan();
                     } else {
-                        if (is_masked(a, b, it)) continue;
+                        if (masked(a, it)) continue;
                         keys[len++] = key;
                         if (len == k) rescan();
                     }
@@ -240,8 +305,6 @@ struct WaveTopK {
     }
 };
 
-// LDS bytes of the per-wave lists: keys [32][k] u64 + meta [32][2] i32
-__host__ __device__ constexpr size_t list_bytes_per_wave(int k) { return (size_t)kUsersPerWave * (k * 8 + 8); }
 
 template <int DT, int KCH, bool MINMAX>
 __global__ __launch_bounds__(256) void score_topk_kernel(ScoreArgs a) {
@@ -251,7 +314,7 @@ __global__ __launch_bounds__(256) void score_topk_kernel(ScoreArgs a) {
     const int h = lane >> 5, col = lane & 31;
     const int k = a.k;
     uint64_t* lk = reinterpret_cast<uint64_t*>(smem + (size_t)wave * list_bytes_per_wave(k));
-    int32_t* lm = reinterpret_cast<int32_t*>(lk + (size_t)kUsersPerWave * k);
+    int32_t* lm = reinterpret_cast<int32_t*>(lk + (size_t)kUsersPerWave * kstride(k) + kListSpare);
 
     const int64_t b = (int64_t)blockIdx.x * kUsersPerBlock + wave * kUsersPerWave + col;  // this lane's user
     const bool user_ok = b < a.B;
@@ -259,8 +322,9 @@ __global__ __launch_bounds__(256) void score_topk_kernel(ScoreArgs a) {
     typename F::chunk uf[KCH];
 #pragma unroll
     for (int c = 0; c < KCH; ++c) uf[c] = F::load(a.Q, qrow, a.d, c, h, user_ok);
-    WaveTopK st;
+    WaveTopK<64> st;
     st.init(lk, lm, k, lane, b, user_ok);
+    st.build_bloom(a);
 
     const int split = blockIdx.y;
     const int64_t i_begin = (int64_t)split * a.split_items;
@@ -304,7 +368,7 @@ struct LdsGeom {
     static constexpr int SWZ = (CPR < 16 ? CPR : 16) - 1;
 };
 
-template <int KSTEPS, bool MINMAX, bool ABLATE = false>
+template <int KSTEPS, bool MINMAX, int ABLATE = 0>
 __global__ __launch_bounds__(512) void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles) {
     typedef LdsGeom<KSTEPS> G;
     typedef Frag<LGX_DTYPE_BF16> F;
@@ -314,7 +378,7 @@ __global__ __launch_bounds__(512) void score_topk_bf16_lds(ScoreArgs a, int xcd_
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, col = lane & 31;
     uint64_t* lk = reinterpret_cast<uint64_t*>(smem + 2 * G::TILE + (size_t)wave * list_bytes_per_wave(k));
-    int32_t* lm = reinterpret_cast<int32_t*>(lk + (size_t)kUsersPerWave * k);
+    int32_t* lm = reinterpret_cast<int32_t*>(lk + (size_t)kUsersPerWave * kstride(k) + kListSpare);
 
     // workgroup -> (catalog split, user tile)
     const int64_t bid = blockIdx.x;
@@ -337,8 +401,9 @@ __global__ __launch_bounds__(512) void score_topk_bf16_lds(ScoreArgs a, int xcd_
     typename F::chunk uf[KSTEPS];
 #pragma unroll
     for (int c = 0; c < KSTEPS; ++c) uf[c] = F::load(a.Q, qrow, a.d, c, h, user_ok);
-    WaveTopK st;
+    WaveTopK<32> st;
     st.init(lk, lm, k, lane, b, user_ok);
+    st.build_bloom(a);
 
     const int64_t i_begin = (int64_t)split * a.split_items;
     const int64_t i_end = min(a.n_items, i_begin + a.split_items);
@@ -392,11 +457,14 @@ __global__ __launch_bounds__(512) void score_topk_bf16_lds(ScoreArgs a, int xcd_
             acc0 = F::mma(a0, uf[c], acc0);
             acc1 = F::mma(a1, uf[c], acc1);
         }
-        if (ABLATE) {  // development: MFMA + LDS pipeline only (keeps the accumulators live)
+        if (ABLATE == 1) {  // development: MFMA + LDS pipeline only (keeps the accumulators live)
             float z = 0.0f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) z += acc0[r] + acc1[r];
             st.mx = fmaxf(st.mx, z);
+        } else if (ABLATE == 3) {  // development: filter fast path only
+            st.template tile<MINMAX, true, true>(a, acc0, t0, i_end);
+            st.template tile<MINMAX, true, true>(a, acc1, t0 + 32, i_end);
         } else {
             if (t0 + kTileItems <= i_end) {
                 st.template tile<MINMAX, true>(a, acc0, t0, i_end);
@@ -549,7 +617,7 @@ __device__ __forceinline__ void ring_stage(unsigned char* slot, const unsigned c
     }
 }
 
-template <int KSTEPS, bool MINMAX, bool ABLATE = false>
+template <int KSTEPS, bool MINMAX, int ABLATE = 0>
 __global__ __launch_bounds__(512) void score_topk_bf16_ring(ScoreArgs a, int xcd_affine, int64_t n_utiles,
                                                             int* err) {
     typedef RingGeom<KSTEPS> G;
@@ -563,7 +631,7 @@ __global__ __launch_bounds__(512) void score_topk_bf16_ring(ScoreArgs a, int xcd
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, col = lane & 31;
     uint64_t* lk = reinterpret_cast<uint64_t*>(lists + (size_t)wave * list_bytes_per_wave(k));
-    int32_t* lm = reinterpret_cast<int32_t*>(lk + (size_t)kUsersPerWave * k);
+    int32_t* lm = reinterpret_cast<int32_t*>(lk + (size_t)kUsersPerWave * kstride(k) + kListSpare);
 
     const int64_t bid = blockIdx.x;
     int split;
@@ -585,8 +653,9 @@ __global__ __launch_bounds__(512) void score_topk_bf16_ring(ScoreArgs a, int xcd
     typename F::chunk uf[KSTEPS];
 #pragma unroll
     for (int c = 0; c < KSTEPS; ++c) uf[c] = F::load(a.Q, qrow, a.d, c, h, user_ok);
-    WaveTopK st;
+    WaveTopK<32> st;
     st.init(lk, lm, k, lane, b, user_ok);
+    st.build_bloom(a);
 
     const int64_t i_begin = (int64_t)split * a.split_items;
     const int64_t i_end = min(a.n_items, i_begin + a.split_items);
@@ -615,24 +684,34 @@ __global__ __launch_bounds__(512) void score_topk_bf16_ring(ScoreArgs a, int xcd
     __syncthreads();
 
     int64_t next_share = pro;  // next tile this wave owes a share to
-    int64_t pend_lo = pro, pend_hi = pro;  // issued, not yet published: tiles [pend_lo, pend_hi)
-    // publish landed shares, then issue every share the done counters allow
+    int64_t pend_lo = pro, pend_hi = pro;  // issued in an EARLIER service call, not yet published
+    // One service call: (1) issue up to two newly allowed shares, (2) retire the shares issued by
+    // the previous call with a COUNTED wait that leaves the new ones in flight, (3) publish them.
+    // A share's DMA therefore gets one whole iteration to land before anyone waits on it.
     auto service = [&]() {
-        if (pend_lo < pend_hi) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0)
-                for (int64_t q = pend_lo; q < pend_hi; ++q)
-                    __hip_atomic_fetch_add(&filled[q % kRingSlots], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            pend_lo = pend_hi;
-        }
-        while (next_share < ntiles) {
+        int n_new = 0;
+        const int64_t new_lo = next_share;
+        while (n_new < 2 && next_share < ntiles) {
             const int s = (int)(next_share % kRingSlots);
             const int need = kLdsWaves * (int)(next_share / kRingSlots);
             if (__hip_atomic_load(&done[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) break;
             if (p0 < p1) ring_stage<G>(ring + s * G::SLOT, items, tile_start(next_share), i_end, p0, p1, lane);
             ++next_share;
-            pend_hi = next_share;
+            ++n_new;
         }
+        if (pend_lo < pend_hi) {
+            const int inflight = (p1 > p0 ? p1 - p0 : 0) * n_new;  // DMA instructions just issued
+            if (inflight == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else if (inflight == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+            else if (inflight == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            else if (inflight == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            if (lane == 0)
+                for (int64_t q = pend_lo; q < pend_hi; ++q)
+                    __hip_atomic_fetch_add(&filled[q % kRingSlots], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        pend_lo = new_lo;
+        pend_hi = next_share;
     };
 
     bool ok = true;
@@ -650,10 +729,12 @@ __global__ __launch_bounds__(512) void score_topk_bf16_ring(ScoreArgs a, int xcd
         return true;
     };
     for (int64_t t = 0; t < ntiles && ok; t += 2) {
-        service();
         const bool two = t + 1 < ntiles;
-        ok = wait_tile(t) && (!two || wait_tile(t + 1));
-        if (!ok) break;
+        if (ABLATE != 2) {  // ABLATE == 2 (development): resident slots only, no refills / waits
+            service();
+            ok = wait_tile(t) && (!two || wait_tile(t + 1));
+            if (!ok) break;
+        }
         const int s0 = (int)(t % kRingSlots), s1 = (int)((two ? t + 1 : t) % kRingSlots);
         const unsigned char* T0 = ring + s0 * G::SLOT + col * G::RB;
         const unsigned char* T1 = ring + s1 * G::SLOT + col * G::RB;
@@ -685,7 +766,7 @@ __global__ __launch_bounds__(512) void score_topk_bf16_ring(ScoreArgs a, int xcd
         }
         // every fragment read of the pair has returned (the MFMAs consumed them): release
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) {
+        if (lane == 0 && ABLATE != 2) {
             __hip_atomic_fetch_add(&done[s0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (two) __hip_atomic_fetch_add(&done[s1], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
@@ -705,7 +786,7 @@ __global__ __launch_bounds__(512) void score_topk_bf16_ring(ScoreArgs a, int xcd
     }
     // remaining obligations: shares of tiles other waves still need
     uint32_t spins = 0;
-    while (ok && (next_share < ntiles || pend_lo < pend_hi)) {
+    while (ABLATE != 2 && ok && (next_share < ntiles || pend_lo < pend_hi)) {
         service();
         if (next_share < ntiles) {
             if (++spins > kSpinLimit) {
@@ -785,7 +866,7 @@ int launch_v1(const ScoreArgs& a, int kch, hipStream_t stream) {
     return LGX_OK;
 }
 
-template <bool MM, bool ABL = false>
+template <bool MM, int ABL = 0>
 int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     const int ksteps = (int)(a.d / 16);
     const unsigned grid = (unsigned)(p.n_utiles * p.n_splits);
@@ -814,7 +895,7 @@ int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     return LGX_OK;
 }
 
-template <bool MM, bool ABL = false>
+template <bool MM, int ABL = 0>
 int launch_ring(const ScoreArgs& a, const SplitPlan& p, int* err, hipStream_t stream) {
     const int ksteps = (int)(a.d / 16);
     const unsigned grid = (unsigned)(p.n_utiles * p.n_splits);
@@ -894,14 +975,20 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
     }
     const bool mm = minmax_out != nullptr;
     int rc;
-    // development switches: LGX_SCORE_ABLATE=1 (pipeline only), LGX_SCORE_KERNEL=barrier (A/B)
-    static const bool ablate = getenv("LGX_SCORE_ABLATE") && getenv("LGX_SCORE_ABLATE")[0] == '1';
-    static const bool barrier = getenv("LGX_SCORE_KERNEL") && getenv("LGX_SCORE_KERNEL")[0] == 'b';
+    // development switches (A/B and ablation only): LGX_SCORE_KERNEL=ring selects the decoupled
+    // ring kernel; LGX_SCORE_ABLATE=1 drops the top-k work, =3 the mask path (timing studies)
+    static const char* abl_env = getenv("LGX_SCORE_ABLATE");
+    static const bool ablate = abl_env && abl_env[0] == '1';
+    static const bool ablate2 = abl_env && abl_env[0] == '2';
+    static const bool ablate3 = abl_env && abl_env[0] == '3';
+    static const bool ring = getenv("LGX_SCORE_KERNEL") && getenv("LGX_SCORE_KERNEL")[0] == 'r';
     int* err = reinterpret_cast<int*>(base + 2 * list_bytes + 256);
-    if (p.lds && ablate && barrier) rc = launch_lds<false, true>(a, p, stream);
-    else if (p.lds && ablate) rc = launch_ring<false, true>(a, p, err, stream);
-    else if (p.lds && barrier) rc = mm ? launch_lds<true>(a, p, stream) : launch_lds<false>(a, p, stream);
-    else if (p.lds) rc = mm ? launch_ring<true>(a, p, err, stream) : launch_ring<false>(a, p, err, stream);
+    if (p.lds && ablate && ring) rc = launch_ring<false, 1>(a, p, err, stream);
+    else if (p.lds && ablate2 && ring) rc = launch_ring<false, 2>(a, p, err, stream);
+    else if (p.lds && ablate) rc = launch_lds<false, 1>(a, p, stream);
+    else if (p.lds && ablate3) rc = launch_lds<false, 3>(a, p, stream);
+    else if (p.lds && ring) rc = mm ? launch_ring<true>(a, p, err, stream) : launch_ring<false>(a, p, err, stream);
+    else if (p.lds) rc = mm ? launch_lds<true>(a, p, stream) : launch_lds<false>(a, p, stream);
     else if (dtype == LGX_DTYPE_F32) rc = mm ? launch_v1<LGX_DTYPE_F32, true>(a, kch, stream)
                                              : launch_v1<LGX_DTYPE_F32, false>(a, kch, stream);
     else rc = mm ? launch_v1<LGX_DTYPE_BF16, true>(a, kch, stream) : launch_v1<LGX_DTYPE_BF16, false>(a, kch, stream);
