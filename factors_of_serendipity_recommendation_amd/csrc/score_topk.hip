@@ -30,8 +30,28 @@
 namespace lgx {
 namespace {
 
+// Development statistics (tools/score_stats.hip defines LGX_SCORE_STATS; the library never does):
+// per-wave counters and s_memtime cycle stamps, summed into a device array at the end.
+#ifdef LGX_SCORE_STATS
+__device__ unsigned long long g_score_stats[8];
+#define LGX_STAT_DECL uint64_t stat_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define LGX_STAT(i, v) (stat_[i] += (v))
+#define LGX_STAT_T0 const uint64_t stat_t0_ = __builtin_amdgcn_s_memtime();
+#define LGX_STAT_T1(i) LGX_STAT(i, __builtin_amdgcn_s_memtime() - stat_t0_);
+#define LGX_STAT_FLUSH                                                                                 \
+    if ((threadIdx.x & 63) == 0)                                                                       \
+        for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_score_stats[i_], (unsigned long long)stat_[i_]);
+#else
+#define LGX_STAT_DECL
+#define LGX_STAT(i, v)
+#define LGX_STAT_T0
+#define LGX_STAT_T1(i)
+#define LGX_STAT_FLUSH
+#endif
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWavesPerBlock = 4;
 constexpr int kUsersPerWave = 32;
@@ -108,29 +128,44 @@ __device__ __forceinline__ bool is_masked(const ScoreArgs& a, int64_t b, int32_t
 // output row (item offset inside the 32-item tile) of accumulator register r for lane half h
 __device__ __forceinline__ int tile_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-// LDS bytes of the per-wave lists: keys [32][kstride] u64 + meta [32][2] i32 (16-B aligned rows,
-// plus one spare row so the vectorised rescan of the last user stays inside the allocation)
+// LDS bytes of the per-wave lists: keys [32][kstride] u64 (16-B aligned rows, plus spare keys so
+// that the vectorised rescan of user 31 stays inside the allocation), then the deferred-candidate
+// slots [64 lanes][kPendSlots] u64
 __host__ __device__ constexpr int kstride(int k) { return (k + 1) & ~1; }
 constexpr int kListSpare = 8;  // the 8-key rescan of user 31 may read past its row
+constexpr int kPendSlots = 4;
+__host__ __device__ constexpr size_t list_keys_per_wave(int k) { return (size_t)kUsersPerWave * kstride(k) + kListSpare; }
 __host__ __device__ constexpr size_t list_bytes_per_wave(int k) {
-    return ((size_t)kUsersPerWave * kstride(k) + kListSpare) * 8 + kUsersPerWave * 8;
+    return (list_keys_per_wave(k) + 64 * kPendSlots) * 8;
+}
+
+// value held by lane (lane ^ 32): one v_permlane32_swap, no LDS traffic
+__device__ __forceinline__ uint32_t other_half(uint32_t x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return (threadIdx.x & 32) ? r[0] : r[1];
 }
 
 // Running top-k of the 32 users of one wave (lanes col and col+32 share user col).  User col's
-// list is an UNSORTED array of k packed keys in LDS (wave_topk.h key order) plus {len, argmin};
-// the lane mirrors the worst kept entry (tau, tau_i) in registers for the per-score filter.  An
-// accepted candidate overwrites the worst entry and the new worst is found by one scan of k
-// independent LDS reads -- no dependent shift chain.  Lists are sorted only when merged.
-template <int KMAX>
+// list is an UNSORTED array of k packed keys in LDS (wave_topk.h key order); its length, the slot
+// of its worst entry and that entry's key live in registers, identical in both lanes of the user.
+// The lane mirrors the worst kept entry (tau, tau_i) for the per-score filter.  An accepted
+// candidate overwrites the worst entry and the new worst is found by one scan of k independent
+// LDS reads -- no dependent shift chain.  Lists are sorted only when merged.
 struct WaveTopK {
     uint64_t* keys;  // this lane's user: [k]
-    int32_t* meta;   // this lane's user: {len, argmin}
-    int k, col, h;
+    int k, h;
     int64_t b;       // query index of this lane's user
     bool user_ok;
-    float tau;
+    int len, mp;     // list length, slot of the worst entry (valid when len == k)
+    uint64_t kmin;   // worst kept key (valid when len == k)
+    // deferred candidates of THIS lane (its half's items), inserted into the list in batches so
+    // that a late-sweep survivor costs a few register moves instead of LDS round trips
+    static constexpr int kPend = kPendSlots;
+    LGX_STAT_DECL
+    uint64_t* pend;  // this lane's kPend slots in LDS
+    int pcnt;
+    float tau;       // filter threshold: -inf until the list is full, +inf for padding users
     int32_t tau_i;
-    bool full;
     float mn, mx;
     // 256-bit Bloom filter of the user's masked items (2 hashes), as 8 scalars so that the
     // word select stays in registers
@@ -170,23 +205,19 @@ struct WaveTopK {
         }
     }
 
-    __device__ __forceinline__ void init(uint64_t* keys_w, int32_t* meta_w, int k_, int lane, int64_t b_, bool ok) {
+    __device__ __forceinline__ void init(uint64_t* keys_w, uint64_t* pend_w, int k_, int lane, int64_t b_, bool ok) {
         k = k_;
-        col = lane & 31;
         h = lane >> 5;
         b = b_;
         user_ok = ok;
-        keys = keys_w + col * kstride(k);
-        meta = meta_w + col * 2;
-        if (h == 0) {
-            meta[0] = 0;
-            meta[1] = 0;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+        keys = keys_w + (lane & 31) * kstride(k);
+        len = 0;
+        mp = 0;
+        kmin = 0;
+        pend = pend_w + lane * kPend;
+        pcnt = 0;
         tau = ok ? -INFINITY : INFINITY;  // padding users never produce candidates
         tau_i = 0x7fffffff;
-        full = false;
         mn = INFINITY;
         mx = -INFINITY;
     }
@@ -194,96 +225,219 @@ struct WaveTopK {
     // new worst entry: 8 keys (four 16-byte reads issued together) per LDS round trip
     __device__ __forceinline__ void rescan() {
         uint64_t m = ~0ull;
-        int mp = 0;
+        int p = 0;
         for (int j0 = 0; j0 < k; j0 += 8) {
             uint64_t v[8];
 #pragma unroll
             for (int j = 0; j < 8; j += 2) {
-                const ulonglong2 p = *reinterpret_cast<const ulonglong2*>(keys + j0 + j);
-                v[j] = p.x;
-                v[j + 1] = p.y;
+                const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(keys + j0 + j);
+                v[j] = q.x;
+                v[j + 1] = q.y;
             }
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const uint64_t x = (j0 + j < k) ? v[j] : ~0ull;
                 if (x < m) {
                     m = x;
-                    mp = j0 + j;
+                    p = j0 + j;
                 }
             }
         }
-        meta[1] = mp;
+        mp = p;
+        kmin = m;
     }
 
-    // consume one 32-item accumulator tile whose item rows start at i0 (items >= i_end ignored).
-    // Fast path: ONE compare per score against tau (-inf until the list is full, +inf for padding
-    // users), OR-ed into a wave-wide flag; only a tile with a survivor re-tests exactly (bounds,
-    // index tie-break) and inserts.  FULL: the whole 32-item tile is inside [i0, i_end).
-    template <bool MINMAX, bool FULL, bool FASTONLY = false>
-    __device__ __forceinline__ void tile(const ScoreArgs& a, const f32x16& acc, int64_t i0, int64_t i_end) {
-        bool any = false;
+    // consume NACC (1 or 2) 32-item accumulator tiles; tile j's item rows start at i0 + 32 j
+    // (items >= i_end ignored).  Fast path: a max tree and ONE compare per lane against tau,
+    // OR-ed into a wave-wide flag.  Rows past i_end (tail block only) are set to -inf first.
+    template <bool MINMAX, int NACC, bool FASTONLY = false>
+    __device__ __forceinline__ void block(const ScoreArgs& a, f32x16 acc0, f32x16 acc1, int64_t i0, int64_t i_end) {
+        const int64_t ib = i0 + 4 * h;  // item of accumulator row 0 of this lane half
+        const bool tail = i0 + 32 * NACC > i_end;
+        const int64_t rem64 = i_end - ib;
+        const int32_t rem = rem64 > (1 << 30) ? (1 << 30) : (int32_t)rem64;  // offsets < rem are items
+        if (tail) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float s = acc[r];
-            const bool in = FULL || (i0 + tile_row(r, h)) < i_end;
-            if (MINMAX && in && user_ok) {
-                mn = fminf(mn, s);
-                mx = fmaxf(mx, s);
+            for (int r = 0; r < 16; ++r) {
+                if (row_off(0, r) >= rem) acc0[r] = -INFINITY;
+                if (NACC == 2 && row_off(1, r) >= rem) acc1[r] = -INFINITY;
             }
-            any |= in && s >= tau;
+        }
+        float m = acc0[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) m = fmaxf(m, acc0[r]);
+        if (NACC == 2) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) m = fmaxf(m, acc1[r]);
+        }
+        if (MINMAX && user_ok) {
+            float lo = INFINITY;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                lo = fminf(lo, acc0[r] == -INFINITY ? INFINITY : acc0[r]);
+                if (NACC == 2) lo = fminf(lo, acc1[r] == -INFINITY ? INFINITY : acc1[r]);
+            }
+            mn = fminf(mn, lo);
+            mx = fmaxf(mx, m);
         }
         if (FASTONLY) {  // development ablation: filter only
-            mn = fminf(mn, __ballot(any) ? 1.0f : 0.0f);
+            mn = fminf(mn, __ballot(m >= tau) ? 1.0f : 0.0f);
             return;
         }
-        if (__ballot(any) == 0ull) return;  // wave-uniform fast path
+        if (__ballot(m >= tau) == 0ull) return;  // wave-uniform fast path
+        LGX_STAT(1, 1);
+#ifdef LGX_SCORE_STATS
+        const uint64_t ev_t0 = __builtin_amdgcn_s_memtime();
+#endif
+        slow<NACC>(a, acc0, acc1, ib, rem);
+#ifdef LGX_SCORE_STATS
+        stat_[7] += __builtin_amdgcn_s_memtime() - ev_t0;
+#endif
+    }
+
+    __device__ __forceinline__ static int32_t row_off(int j, int r) { return 32 * j + (r & 3) + 8 * (r >> 2); }
+
+    template <int NACC>
+    __device__ __forceinline__ void slow(const ScoreArgs& a, const f32x16& acc0, const f32x16& acc1, int64_t ib,
+                                         int32_t rem) {
+        if (__ballot(len < k) != 0ull) {  // a list is still filling (first block): exact inserts
+            LGX_STAT(3, 1);
+            drain(a);
+            insert_now<NACC>(a, acc0, acc1, ib, survivors<NACC>(acc0, acc1, ib, rem));
+            return;
+        }
+        // every list is full: defer each survivor into this lane's slots.  One compare per score,
+        // the exact index tie-break only inside the (rarely taken) branch
+        const int64_t l64 = (int64_t)tau_i - ib;
+        const int32_t lim = l64 > (1 << 30) ? (1 << 30) : l64 < -1 ? -1 : (int32_t)l64;
+        uint32_t ovf = 0;
+#pragma unroll
+        for (int j = 0; j < NACC; ++j) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float sc = j ? acc1[r] : acc0[r];
+                if (sc >= tau) {
+                    const int32_t off = row_off(j, r);
+                    if (sc > tau || off < lim) {
+                        if (pcnt < kPend) pend[pcnt++] = make_key(sc, (int32_t)ib + off);
+                        else ovf |= 1u << (16 * j + r);
+                    }
+                }
+            }
+        }
+        if (__ballot(ovf != 0u) != 0ull) {  // slots full: drain, then insert the rest exactly
+            LGX_STAT(2, 1);
+            drain(a);
+            insert_now<NACC>(a, acc0, acc1, ib, ovf & survivors<NACC>(acc0, acc1, ib, rem));
+        }
+    }
+
+    __device__ __forceinline__ int32_t item_of(int64_t ib, int r) const {
+        return (int32_t)ib + row_off(r >> 4, r & 15);
+    }
+    template <int NACC>
+    __device__ __forceinline__ static float pick(const f32x16& acc0, const f32x16& acc1, int r) {
+        float sc = acc0[0];
+#pragma unroll
+        for (int q = 1; q < 16; ++q) sc = ((r & 15) == q) ? acc0[q] : sc;
+        if (NACC == 2 && r >= 16) {
+            sc = acc1[0];
+#pragma unroll
+            for (int q = 1; q < 16; ++q) sc = ((r & 15) == q) ? acc1[q] : sc;
+        }
+        return sc;
+    }
+    // exact survivors of a block against the current list (bounds, index tie-break), branch-free;
+    // item tests are relative to the lane's first item so the per-score offsets are constants
+    template <int NACC>
+    __device__ __forceinline__ uint32_t survivors(const f32x16& acc0, const f32x16& acc1, int64_t ib,
+                                                  int32_t rem) const {
+        const bool notfull = len < k;
+        const int64_t l64 = (int64_t)tau_i - ib;
+        const int32_t lim = l64 > (1 << 30) ? (1 << 30) : l64 < -1 ? -1 : (int32_t)l64;
         uint32_t cmask = 0;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int32_t it = (int32_t)(i0 + tile_row(r, h));
-            if (user_ok && it < i_end && (!full || better(acc[r], it, tau, tau_i))) cmask |= 1u << r;
+        for (int j = 0; j < NACC; ++j) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float sc = j ? acc1[r] : acc0[r];
+                const int32_t off = row_off(j, r);
+                const bool beats = notfull | (sc > tau) | ((sc == tau) & (off < lim));
+                cmask |= (user_ok & (off < rem) & beats) ? (1u << (16 * j + r)) : 0u;
+            }
         }
-        // the two lane halves hold different items of the same 32 users -> serialise them
+        return cmask;
+    }
+
+    // one candidate into this lane's user list (the caller serialises the two lane halves)
+    __device__ __forceinline__ void insert_key(const ScoreArgs& a, uint64_t key) {
+        const int32_t it = key_index(key);
+        if (len == k) {
+            if (key <= kmin || masked(a, it)) return;
+            keys[mp] = key;
+            rescan();
+        } else {
+            if (masked(a, it)) return;
+            keys[len++] = key;
+            if (len == k) rescan();
+        }
+    }
+    // after half ph changed the list: the other half adopts {len, mp, kmin} (cross-half swap)
+    __device__ __forceinline__ void sync_from(int ph) {
+        __builtin_amdgcn_wave_barrier();  // list writes of half ph precede the other half's reads
+        const uint32_t lm = other_half((uint32_t)len | ((uint32_t)mp << 16));
+        const uint32_t klo = other_half((uint32_t)kmin), khi = other_half((uint32_t)(kmin >> 32));
+        if (ph != h) {
+            len = (int)(lm & 0xffffu);
+            mp = (int)(lm >> 16);
+            kmin = ((uint64_t)khi << 32) | klo;
+        }
+    }
+    __device__ __forceinline__ void refresh_tau() {
+        if (len == k && user_ok) {
+            tau = key_score(kmin);
+            tau_i = key_index(kmin);
+        }
+    }
+    // insert every deferred candidate of the wave (both halves, serialised)
+    __device__ __forceinline__ void drain(const ScoreArgs& a) {
+        for (int ph = 0; ph < 2; ++ph) {
+            if (__ballot(ph == h && pcnt > 0) == 0ull) continue;
+            if (ph == h) {
+                for (int j = 0; j < pcnt; ++j) insert_key(a, pend[j]);
+                pcnt = 0;
+            }
+            sync_from(ph);
+        }
+        refresh_tau();
+    }
+    // insert a block's survivors directly (pending list already drained)
+    template <int NACC>
+    __device__ __forceinline__ void insert_now(const ScoreArgs& a, const f32x16& acc0, const f32x16& acc1, int64_t ib,
+                                               uint32_t cmask) {
         for (int ph = 0; ph < 2; ++ph) {
             if (__ballot(ph == h && cmask != 0) == 0ull) continue;
-            if (ph == h && cmask) {
-                int len = meta[0];
+            if (ph == h) {
                 uint32_t todo = cmask;
                 while (todo) {  // one copy of the insertion code, one iteration per survivor
                     const int r = __builtin_ctz(todo);
                     todo &= todo - 1;
-                    float sc = acc[0];
-#pragma unroll
-                    for (int q = 1; q < 16; ++q) sc = (r == q) ? acc[q] : sc;
-                    const int32_t it = (int32_t)(i0 + tile_row(r, h));
-                    const uint64_t key = make_key(sc, it);
-                    if (len == k) {
-                        const int mp = meta[1];
-                        if (key <= keys[mp] || masked(a, it)) continue;
-                        keys[mp] = key;
-                        rescan();
-                    } else {
-                        if (masked(a, it)) continue;
-                        keys[len++] = key;
-                        if (len == k) rescan();
-                    }
+                    insert_key(a, make_key(pick<NACC>(acc0, acc1, r), item_of(ib, r)));
                 }
-                meta[0] = len;
             }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
+            sync_from(ph);
         }
-        full = meta[0] == k;
-        if (full && user_ok) {
-            const uint64_t m = keys[meta[1]];
-            tau = key_score(m);
-            tau_i = key_index(m);
-        }
+        refresh_tau();
+    }
+
+    template <bool MINMAX>
+    __device__ __forceinline__ void tile(const ScoreArgs& a, const f32x16& acc, int64_t i0, int64_t i_end) {
+        block<MINMAX, 1>(a, acc, acc, i0, i_end);
     }
 
     __device__ __forceinline__ void flush(const ScoreArgs& a, int split, int lane) {
+        drain(a);
         if (user_ok && h == 0) {
-            const int len = meta[0];
             float* ps = a.part_score + ((size_t)b * a.n_splits + split) * k;
             int32_t* pi = a.part_idx + ((size_t)b * a.n_splits + split) * k;
             for (int j = 0; j < k; ++j) {
@@ -314,7 +468,6 @@ __global__ __launch_bounds__(256) void score_topk_kernel(ScoreArgs a) {
     const int h = lane >> 5, col = lane & 31;
     const int k = a.k;
     uint64_t* lk = reinterpret_cast<uint64_t*>(smem + (size_t)wave * list_bytes_per_wave(k));
-    int32_t* lm = reinterpret_cast<int32_t*>(lk + (size_t)kUsersPerWave * kstride(k) + kListSpare);
 
     const int64_t b = (int64_t)blockIdx.x * kUsersPerBlock + wave * kUsersPerWave + col;  // this lane's user
     const bool user_ok = b < a.B;
@@ -322,8 +475,8 @@ __global__ __launch_bounds__(256) void score_topk_kernel(ScoreArgs a) {
     typename F::chunk uf[KCH];
 #pragma unroll
     for (int c = 0; c < KCH; ++c) uf[c] = F::load(a.Q, qrow, a.d, c, h, user_ok);
-    WaveTopK<64> st;
-    st.init(lk, lm, k, lane, b, user_ok);
+    WaveTopK st;
+    st.init(lk, lk + list_keys_per_wave(k), k, lane, b, user_ok);
     st.build_bloom(a);
 
     const int split = blockIdx.y;
@@ -340,15 +493,14 @@ __global__ __launch_bounds__(256) void score_topk_kernel(ScoreArgs a) {
             const typename F::chunk ia = F::load(a.items, item_row, a.d, c, h, item_ok);
             acc = F::mma(ia, uf[c], acc);
         }
-        if (i0 + 32 <= i_end) st.template tile<MINMAX, true>(a, acc, i0, i_end);
-        else st.template tile<MINMAX, false>(a, acc, i0, i_end);
+        st.template tile<MINMAX>(a, acc, i0, i_end);
     }
     st.flush(a, split, lane);
 }
 
 // ---------------------------------------------------------------------------- bf16 LDS kernel
 // 512 threads = 8 waves x 32 users; the workgroup streams 64-item tiles of its catalog split
-// through a double-buffered LDS ring filled by LDS-DMA (global_load_lds_dwordx4), so every item
+// through a 2-4 buffer LDS ring filled by LDS-DMA (global_load_lds_dwordx4), so every item
 // byte crosses L2 -> CU once per workgroup and feeds 8 waves.  Rows are stored with their 16-B
 // chunks XOR-swizzled by (item & 15) so the fragment reads (32 items, same chunk) are
 // conflict-free ds_read_b128s; the swizzle is applied to the DMA SOURCE address because the LDS
@@ -365,20 +517,53 @@ struct LdsGeom {
     static constexpr int TILE = kTileItems * RB;        // bytes per tile
     static constexpr int PIECES = TILE / 1024;          // 1-KiB LDS-DMA wave instructions per tile
     static constexpr int PPW = (PIECES + kLdsWaves - 1) / kLdsWaves;
-    static constexpr int SWZ = (CPR < 16 ? CPR : 16) - 1;
+    // XOR swizzle inside aligned groups of P chunks, P = the largest power of two (<= 16)
+    // dividing CPR, so that chunk ^ (row & SWZ) is a permutation of the row's chunks
+    static constexpr int SWZ = ((CPR & -CPR) < 16 ? (CPR & -CPR) : 16) - 1;
 };
 
+// LDS-DMA of one 1-KiB piece: lane l copies 16 B from sbase + voff (its own offset) to LDS byte
+// lds_addr + 16 l.  Issued from inline asm ON PURPOSE: the compiler's wait-count pass cannot tell
+// the tiles of the LDS ring apart and would put an s_waitcnt vmcnt(0) in front of every later LDS
+// read, which serialises the prefetch.  The kernel orders the DMA itself: counted vmcnt (this
+// wave's pieces) + workgroup barrier (everyone's), as the hardware requires.
+__device__ __forceinline__ void lds_dma16(const void* sbase, uint32_t voff, uint32_t lds_addr) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+                 :: "v"(voff), "s"(sbase), "s"(lds_addr) : "memory", "m0");
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (conservative above 15)
+__device__ __forceinline__ void wait_vmcnt_le(int n) {
+#define LGX_VMW(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+    switch (n) {
+        LGX_VMW(1) LGX_VMW(2) LGX_VMW(3) LGX_VMW(4) LGX_VMW(5) LGX_VMW(6) LGX_VMW(7) LGX_VMW(8)
+        LGX_VMW(9) LGX_VMW(10) LGX_VMW(11) LGX_VMW(12) LGX_VMW(13) LGX_VMW(14) LGX_VMW(15)
+        default:
+            if (n >= 16) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+#undef LGX_VMW
+}
+
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// Pipeline: nbuf tile buffers, nbuf-1 tiles in flight.  Iteration t issues tile t+nbuf-1 into the
+// buffer tile t-1 used (every wave left it at the barrier closing t-1), computes tile t, then
+// waits for its own pieces of tile t+1 (vmcnt leaves the younger tiles' pieces in flight) and
+// joins the barrier that publishes tile t+1 to all waves.
 template <int KSTEPS, bool MINMAX, int ABLATE = 0>
-__global__ __launch_bounds__(512) void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles) {
+__global__ __launch_bounds__(512) void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf) {
     typedef LdsGeom<KSTEPS> G;
     typedef Frag<LGX_DTYPE_BF16> F;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    unsigned char* tiles = smem;  // [2][TILE]
+    unsigned char* tiles = smem;  // [nbuf][TILE]
     const int k = a.k;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5, col = lane & 31;
-    uint64_t* lk = reinterpret_cast<uint64_t*>(smem + 2 * G::TILE + (size_t)wave * list_bytes_per_wave(k));
-    int32_t* lm = reinterpret_cast<int32_t*>(lk + (size_t)kUsersPerWave * kstride(k) + kListSpare);
+    uint64_t* lk = reinterpret_cast<uint64_t*>(smem + (size_t)nbuf * G::TILE + (size_t)wave * list_bytes_per_wave(k));
 
     // workgroup -> (catalog split, user tile)
     const int64_t bid = blockIdx.x;
@@ -401,9 +586,19 @@ __global__ __launch_bounds__(512) void score_topk_bf16_lds(ScoreArgs a, int xcd_
     typename F::chunk uf[KSTEPS];
 #pragma unroll
     for (int c = 0; c < KSTEPS; ++c) uf[c] = F::load(a.Q, qrow, a.d, c, h, user_ok);
-    WaveTopK<32> st;
-    st.init(lk, lm, k, lane, b, user_ok);
+    WaveTopK st;
+    st.init(lk, lk + list_keys_per_wave(k), k, lane, b, user_ok);
     st.build_bloom(a);
+    // consume the prologue loads here: otherwise the compiler treats them as possibly pending at
+    // the loop header and waits vmcnt(0) -- i.e. for the tile prefetch -- in every iteration
+#pragma unroll
+    for (int c = 0; c < KSTEPS; ++c) {
+        u32x4 t = __builtin_bit_cast(u32x4, uf[c]);
+        asm volatile("" : "+v"(t));
+        uf[c] = __builtin_bit_cast(uint4, t);
+    }
+    asm volatile("" : "+v"(st.bl0), "+v"(st.bl1), "+v"(st.bl2), "+v"(st.bl3), "+v"(st.bl4), "+v"(st.bl5),
+                 "+v"(st.bl6), "+v"(st.bl7));
 
     const int64_t i_begin = (int64_t)split * a.split_items;
     const int64_t i_end = min(a.n_items, i_begin + a.split_items);
@@ -413,34 +608,44 @@ __global__ __launch_bounds__(512) void score_topk_bf16_lds(ScoreArgs a, int xcd_
     const int64_t rot = a.n_splits == 1 ? (bid % 8) * (ntiles / 8) : 0;
     const unsigned char* items = static_cast<const unsigned char*>(a.items);
 
-    auto stage = [&](int buf, int64_t t0) {
-#pragma unroll
-        for (int p = 0; p < G::PPW; ++p) {
-            const int piece = wave * G::PPW + p;
-            if (piece < G::PIECES) {
-                const int q = piece * 64 + lane;  // 16-B LDS slot written by this lane
-                const int item = q / G::CPR, pch = q % G::CPR;
-                const int src = pch ^ (item & G::SWZ);
-                const int64_t gi = min(t0 + item, i_end - 1);  // tail rows: any valid row, masked later
-                const unsigned char* gp = items + gi * G::RB + src * 16;
-                __builtin_amdgcn_global_load_lds(
-                    gp, (__attribute__((address_space(3))) void*)(tiles + buf * G::TILE + piece * 1024), 16, 0, 0);
-            }
-        }
-    };
+    // this wave's pieces of a tile: LDS slot q = piece*64 + lane holds 16-B chunk (q % CPR) of tile
+    // row q / CPR, fetched from source chunk (q % CPR) ^ (row & SWZ) (the swizzle lives on the source
+    // side because the DMA's LDS destination is lane-linear)
+    const int my_pieces = max(0, min(G::PPW, G::PIECES - wave * G::PPW));
+    const uint32_t lds_tiles = lds_u32(tiles);
 
     auto tile_start = [&](int64_t t) {
         int64_t u = t + rot;
         if (u >= ntiles) u -= ntiles;
         return i_begin + u * kTileItems;
     };
-    if (ntiles > 0) stage(0, tile_start(0));
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    auto stage = [&](int buf, int64_t t0) {
+        const unsigned char* base = items + t0 * G::RB;
+        const bool tail = t0 + kTileItems > i_end;
+        const int last = (int)(i_end - 1 - t0);  // tail rows re-read the split's last row (masked later)
+#pragma unroll
+        for (int p = 0; p < G::PPW; ++p) {
+            if (p < my_pieces) {
+                // offsets recomputed per tile: cheaper than holding them in registers
+                const int q = (wave * G::PPW + p) * 64 + lane;
+                const int row = q / G::CPR;
+                const int src = (q % G::CPR) ^ (row & G::SWZ);
+                const int srow = tail && row > last ? last : row;
+                lds_dma16(base, (uint32_t)(srow * G::RB + src * 16),
+                          __builtin_amdgcn_readfirstlane(lds_tiles + buf * G::TILE + (wave * G::PPW + p) * 1024));
+            }
+        }
+    };
+
+    const int ahead = nbuf - 1;
+    for (int j = 0; j < ahead && j < ntiles; ++j) stage(j, tile_start(j));
+    wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(ahead, ntiles) - 1));
     __syncthreads();
+    int buf = 0, sbuf = ahead;  // buffer of tile t / of tile t + ahead
     for (int64_t t = 0; t < ntiles; ++t) {
-        const int buf = (int)(t & 1);
+        LGX_STAT_T0
         const int64_t t0 = tile_start(t);
-        if (t + 1 < ntiles) stage(buf ^ 1, tile_start(t + 1));
+        if (t + ahead < ntiles) stage(sbuf, tile_start(t + ahead));
         const unsigned char* T = tiles + buf * G::TILE;
         f32x16 acc0, acc1;
 #pragma unroll
@@ -449,35 +654,63 @@ __global__ __launch_bounds__(512) void score_topk_bf16_lds(ScoreArgs a, int xcd_
             acc1[r] = 0.0f;
         }
         const int it0 = col, it1 = 32 + col;
+        const unsigned char* r0 = T + it0 * G::RB;
+        const unsigned char* r1 = T + it1 * G::RB;
+        // fragment reads run one k-step ahead of the MFMAs
+        uint4 a0 = *reinterpret_cast<const uint4*>(r0 + ((h ^ (it0 & G::SWZ)) * 16));
+        uint4 a1 = *reinterpret_cast<const uint4*>(r1 + ((h ^ (it1 & G::SWZ)) * 16));
 #pragma unroll
         for (int c = 0; c < KSTEPS; ++c) {
-            const int pch = 2 * c + h;
-            const uint4 a0 = *reinterpret_cast<const uint4*>(T + it0 * G::RB + ((pch ^ (it0 & G::SWZ)) * 16));
-            const uint4 a1 = *reinterpret_cast<const uint4*>(T + it1 * G::RB + ((pch ^ (it1 & G::SWZ)) * 16));
+            uint4 n0 = a0, n1 = a1;
+            if (c + 1 < KSTEPS) {
+                const int pch = 2 * (c + 1) + h;
+                n0 = *reinterpret_cast<const uint4*>(r0 + ((pch ^ (it0 & G::SWZ)) * 16));
+                n1 = *reinterpret_cast<const uint4*>(r1 + ((pch ^ (it1 & G::SWZ)) * 16));
+            }
             acc0 = F::mma(a0, uf[c], acc0);
             acc1 = F::mma(a1, uf[c], acc1);
+            a0 = n0;
+            a1 = n1;
         }
+        // keep the reads one k-step ahead: 2 DS reads, then the 2 MFMAs of the previous k-step
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+        for (int c = 0; c < KSTEPS; ++c) {
+            if (c + 1 < KSTEPS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        }
+#ifdef LGX_SCORE_STATS
+        const uint64_t stat_t1_ = __builtin_amdgcn_s_memtime();
+#endif
         if (ABLATE == 1) {  // development: MFMA + LDS pipeline only (keeps the accumulators live)
             float z = 0.0f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) z += acc0[r] + acc1[r];
             st.mx = fmaxf(st.mx, z);
         } else if (ABLATE == 3) {  // development: filter fast path only
-            st.template tile<MINMAX, true, true>(a, acc0, t0, i_end);
-            st.template tile<MINMAX, true, true>(a, acc1, t0 + 32, i_end);
+            st.template block<MINMAX, 2, true>(a, acc0, acc1, t0, i_end);
         } else {
-            if (t0 + kTileItems <= i_end) {
-                st.template tile<MINMAX, true>(a, acc0, t0, i_end);
-                st.template tile<MINMAX, true>(a, acc1, t0 + 32, i_end);
-            } else {
-                st.template tile<MINMAX, false>(a, acc0, t0, i_end);
-                st.template tile<MINMAX, false>(a, acc1, t0 + 32, i_end);
-            }
+            st.template block<MINMAX, 2>(a, acc0, acc1, t0, i_end);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef LGX_SCORE_STATS
+        const uint64_t stat_t2_ = __builtin_amdgcn_s_memtime();
+        st.stat_[4] += stat_t2_ - stat_t1_;  // top-k work
+        st.stat_[5] += stat_t1_ - stat_t0_;  // staging + MFMA
+        st.stat_[0] += 1;
+#endif
+        // tiles t+2 .. t+ahead may stay in flight; tile t+1 must have landed
+        wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(t + ahead, ntiles - 1) - (t + 1)));
         __syncthreads();
+#ifdef LGX_SCORE_STATS
+        st.stat_[6] += __builtin_amdgcn_s_memtime() - stat_t2_;  // wait + barrier
+#endif
+        buf = buf + 1 == nbuf ? 0 : buf + 1;
+        sbuf = sbuf + 1 == nbuf ? 0 : sbuf + 1;
     }
     st.flush(a, split, lane);
+#ifdef LGX_SCORE_STATS
+    { uint64_t* stat_ = st.stat_; LGX_STAT_FLUSH }
+#endif
 }
 
 // one wave per query: merge the split lists, masked tail, optional sigmoid
@@ -573,233 +806,6 @@ int kch_for(int dtype, int64_t d) {
     return -1;
 }
 
-// ---------------------------------------------------------------------------- bf16 LDS ring kernel
-// Same data path as score_topk_bf16_lds but without a workgroup barrier per tile: the 8 waves
-// run decoupled over a ring of kRingSlots 32-item slots, so a wave that takes the top-k slow path
-// delays only itself (the ring absorbs up to kRingSlots-1 tiles of drift).
-// Every refill is split into 8 shares (wave w moves pieces [w*PPW, (w+1)*PPW) by LDS-DMA).  Two
-// monotonic LDS counters per slot carry the protocol:
-//   done[s]   += 1 when a wave has finished reading the slot's current tile;
-//   filled[s] += 1 when a wave's share of the slot's next tile has landed (published after that
-//               wave's s_waitcnt vmcnt(0), lazily at its next service point).
-// Tile t lives in slot t % R during occupancy j = t / R: it is readable once filled >= 8(j+1), and
-// a wave may issue its share of tile t once done >= 8 j (everybody finished tile t - R).  Each wave
-// services its obligations (publish landed shares, issue allowed ones) at every tile boundary and
-// inside every wait, so the wave waiting on the oldest tile always makes progress (no deadlock).
-// All spins are bounded (timeout -> error word, sweep abandoned: wrong results, never a hang).
-constexpr int kRingSlots = 6;  // even: a pair of tiles never wraps inside one slot
-constexpr int kRingItems = 32;
-constexpr uint32_t kSpinLimit = 1u << 22;
-
-template <int KSTEPS>
-struct RingGeom {
-    static constexpr int RB = KSTEPS * 32;
-    static constexpr int CPR = RB / 16;
-    static constexpr int SLOT = kRingItems * RB;  // bytes per slot (16 KiB at d = 256)
-    static constexpr int PIECES = SLOT / 1024;    // 1-KiB LDS-DMA instructions per slot
-    static constexpr int PPW = (PIECES + kLdsWaves - 1) / kLdsWaves;
-    static constexpr int SWZ = (CPR < 16 ? CPR : 16) - 1;
-};
-
-// issue the LDS-DMA pieces [p0, p1) of the tile starting at item t0 into one ring slot
-template <typename G>
-__device__ __forceinline__ void ring_stage(unsigned char* slot, const unsigned char* items, int64_t t0, int64_t i_end,
-                                           int p0, int p1, int lane) {
-#pragma unroll 1  // keep the per-piece address math inside the loop (no hoisted live ranges)
-    for (int piece = p0; piece < p1; ++piece) {
-        const int q = piece * 64 + lane;
-        const int item = q / G::CPR, pch = q % G::CPR;
-        const int src = pch ^ (item & G::SWZ);
-        int64_t gi = t0 + item;
-        if (gi > i_end - 1) gi = i_end - 1;  // tail rows: any valid row, masked later
-        const unsigned char* gp = items + gi * G::RB + src * 16;
-        __builtin_amdgcn_global_load_lds(gp, (__attribute__((address_space(3))) void*)(slot + piece * 1024), 16, 0, 0);
-    }
-}
-
-template <int KSTEPS, bool MINMAX, int ABLATE = 0>
-__global__ __launch_bounds__(512) void score_topk_bf16_ring(ScoreArgs a, int xcd_affine, int64_t n_utiles,
-                                                            int* err) {
-    typedef RingGeom<KSTEPS> G;
-    typedef Frag<LGX_DTYPE_BF16> F;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    unsigned char* ring = smem;  // [kRingSlots][SLOT]
-    int* filled = reinterpret_cast<int*>(smem + kRingSlots * G::SLOT);
-    int* done = filled + kRingSlots;
-    unsigned char* lists = smem + kRingSlots * G::SLOT + 2 * kRingSlots * sizeof(int) + 16;
-    const int k = a.k;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int h = lane >> 5, col = lane & 31;
-    uint64_t* lk = reinterpret_cast<uint64_t*>(lists + (size_t)wave * list_bytes_per_wave(k));
-    int32_t* lm = reinterpret_cast<int32_t*>(lk + (size_t)kUsersPerWave * kstride(k) + kListSpare);
-
-    const int64_t bid = blockIdx.x;
-    int split;
-    int64_t utile;
-    if (xcd_affine) {
-        const int64_t per = a.n_splits / 8;
-        const int64_t r = bid / 8;
-        split = (int)(bid % 8 + 8 * (r % per));
-        utile = r / per;
-    } else {
-        split = (int)(bid % a.n_splits);
-        utile = bid / a.n_splits;
-    }
-    if (utile >= n_utiles) return;
-
-    const int64_t b = utile * kLdsUsers + wave * kUsersPerWave + col;
-    const bool user_ok = b < a.B;
-    const int64_t qrow = user_ok ? (a.user_rows ? a.user_rows[b] : b) : 0;
-    typename F::chunk uf[KSTEPS];
-#pragma unroll
-    for (int c = 0; c < KSTEPS; ++c) uf[c] = F::load(a.Q, qrow, a.d, c, h, user_ok);
-    WaveTopK<32> st;
-    st.init(lk, lm, k, lane, b, user_ok);
-    st.build_bloom(a);
-
-    const int64_t i_begin = (int64_t)split * a.split_items;
-    const int64_t i_end = min(a.n_items, i_begin + a.split_items);
-    const int64_t ntiles = i_end > i_begin ? (i_end - i_begin + kRingItems - 1) / kRingItems : 0;
-    // single split: every workgroup sweeps the whole catalog, starting at a rotation shared by the
-    // workgroups of its XCD (blockIdx mod 8) so that co-resident workgroups read the same tiles
-    const int64_t rot = a.n_splits == 1 ? (bid % 8) * (ntiles / 8) : 0;
-    const unsigned char* items = static_cast<const unsigned char*>(a.items);
-    auto tile_start = [&](int64_t t) {
-        int64_t u = t + rot;
-        if (u >= ntiles) u -= ntiles;
-        return i_begin + u * kRingItems;
-    };
-    const int p0 = wave * G::PPW;
-    const int p1 = (p0 + G::PPW < G::PIECES) ? p0 + G::PPW : (int)G::PIECES;
-
-    // prologue: every wave loads its share of the first kRingSlots tiles
-    const int64_t pro = ntiles < kRingSlots ? ntiles : kRingSlots;
-    for (int64_t t = 0; t < pro; ++t)
-        if (p0 < p1) ring_stage<G>(ring + (int)t * G::SLOT, items, tile_start(t), i_end, p0, p1, lane);
-    if (threadIdx.x < kRingSlots) {
-        filled[threadIdx.x] = threadIdx.x < pro ? kLdsWaves : 0;
-        done[threadIdx.x] = 0;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    int64_t next_share = pro;  // next tile this wave owes a share to
-    int64_t pend_lo = pro, pend_hi = pro;  // issued in an EARLIER service call, not yet published
-    // One service call: (1) issue up to two newly allowed shares, (2) retire the shares issued by
-    // the previous call with a COUNTED wait that leaves the new ones in flight, (3) publish them.
-    // A share's DMA therefore gets one whole iteration to land before anyone waits on it.
-    auto service = [&]() {
-        int n_new = 0;
-        const int64_t new_lo = next_share;
-        while (n_new < 2 && next_share < ntiles) {
-            const int s = (int)(next_share % kRingSlots);
-            const int need = kLdsWaves * (int)(next_share / kRingSlots);
-            if (__hip_atomic_load(&done[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) break;
-            if (p0 < p1) ring_stage<G>(ring + s * G::SLOT, items, tile_start(next_share), i_end, p0, p1, lane);
-            ++next_share;
-            ++n_new;
-        }
-        if (pend_lo < pend_hi) {
-            const int inflight = (p1 > p0 ? p1 - p0 : 0) * n_new;  // DMA instructions just issued
-            if (inflight == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            else if (inflight == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-            else if (inflight == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-            else if (inflight == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            if (lane == 0)
-                for (int64_t q = pend_lo; q < pend_hi; ++q)
-                    __hip_atomic_fetch_add(&filled[q % kRingSlots], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        pend_lo = new_lo;
-        pend_hi = next_share;
-    };
-
-    bool ok = true;
-    // tiles are consumed in pairs (two independent MFMA chains, one wait / release / epilogue
-    // branch per 64 items); an odd tail tile is paired with itself and masked out
-    auto wait_tile = [&](int64_t t) {
-        const int s = (int)(t % kRingSlots);
-        const int need = kLdsWaves * (int)(t / kRingSlots + 1);
-        uint32_t spins = 0;
-        while (__hip_atomic_load(&filled[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
-            if (++spins > kSpinLimit) return false;
-            service();
-            __builtin_amdgcn_s_sleep(1);
-        }
-        return true;
-    };
-    for (int64_t t = 0; t < ntiles && ok; t += 2) {
-        const bool two = t + 1 < ntiles;
-        if (ABLATE != 2) {  // ABLATE == 2 (development): resident slots only, no refills / waits
-            service();
-            ok = wait_tile(t) && (!two || wait_tile(t + 1));
-            if (!ok) break;
-        }
-        const int s0 = (int)(t % kRingSlots), s1 = (int)((two ? t + 1 : t) % kRingSlots);
-        const unsigned char* T0 = ring + s0 * G::SLOT + col * G::RB;
-        const unsigned char* T1 = ring + s1 * G::SLOT + col * G::RB;
-        f32x16 acc0, acc1;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            acc0[r] = 0.0f;
-            acc1[r] = 0.0f;
-        }
-        // 2-deep fragment window per chain
-        uint4 fa0[2], fa1[2];
-#pragma unroll
-        for (int c = 0; c < 2 && c < KSTEPS; ++c) {
-            const int off = ((2 * c + h) ^ (col & G::SWZ)) * 16;
-            fa0[c] = *reinterpret_cast<const uint4*>(T0 + off);
-            fa1[c] = *reinterpret_cast<const uint4*>(T1 + off);
-        }
-#pragma unroll
-        for (int c = 0; c < KSTEPS; ++c) {
-            const uint4 c0 = fa0[c & 1], c1 = fa1[c & 1];
-            if (c + 2 < KSTEPS) {
-                const int off = ((2 * (c + 2) + h) ^ (col & G::SWZ)) * 16;
-                fa0[c & 1] = *reinterpret_cast<const uint4*>(T0 + off);
-                fa1[c & 1] = *reinterpret_cast<const uint4*>(T1 + off);
-            }
-            acc0 = F::mma(c0, uf[c], acc0);
-            acc1 = F::mma(c1, uf[c], acc1);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        // every fragment read of the pair has returned (the MFMAs consumed them): release
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0 && ABLATE != 2) {
-            __hip_atomic_fetch_add(&done[s0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (two) __hip_atomic_fetch_add(&done[s1], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        const int64_t ta = tile_start(t);
-        const int64_t tb = two ? tile_start(t + 1) : i_end;  // tb = i_end: tile fully masked
-        if (ABLATE) {  // development: pipeline only
-            float z = 0.0f;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) z += acc0[r] + acc1[r];
-            st.mx = fmaxf(st.mx, z);
-        } else {
-            if (ta + kRingItems <= i_end) st.template tile<MINMAX, true>(a, acc0, ta, i_end);
-            else st.template tile<MINMAX, false>(a, acc0, ta, i_end);
-            if (tb + kRingItems <= i_end) st.template tile<MINMAX, true>(a, acc1, tb, i_end);
-            else st.template tile<MINMAX, false>(a, acc1, tb, i_end);
-        }
-    }
-    // remaining obligations: shares of tiles other waves still need
-    uint32_t spins = 0;
-    while (ABLATE != 2 && ok && (next_share < ntiles || pend_lo < pend_hi)) {
-        service();
-        if (next_share < ntiles) {
-            if (++spins > kSpinLimit) {
-                ok = false;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    if (!ok && lane == 0) atomicExch(err, 1);
-    st.flush(a, split, lane);
-}
-
 struct SplitPlan {
     int n_splits;
     int64_t split_items;
@@ -808,9 +814,10 @@ struct SplitPlan {
     int64_t n_utiles;
 };
 
-// LDS kernel applies to bf16, d a multiple of 16 up to 256, k <= 32 (LDS budget)
+// LDS kernel applies to bf16, d a multiple of 32 up to 256 (even k-step counts are instantiated),
+// k <= 32 (LDS budget)
 bool lds_eligible(int dtype, int64_t d, int k) {
-    return dtype == LGX_DTYPE_BF16 && d % 16 == 0 && d >= 32 && d <= 256 && k <= 32;
+    return dtype == LGX_DTYPE_BF16 && d % 32 == 0 && d >= 32 && d <= 256 && k <= 32;
 }
 
 SplitPlan plan_splits(int64_t B, int64_t n_items, int dtype, int64_t d, int k) {
@@ -866,16 +873,26 @@ int launch_v1(const ScoreArgs& a, int kch, hipStream_t stream) {
     return LGX_OK;
 }
 
+// tile buffers of the barrier kernel: as many as fit beside the top-k lists, 2..4
+constexpr size_t kLdsBytes = 160 * 1024;
+inline int lds_ring_buffers(size_t tile, size_t lists) {
+    const size_t fit = lists < kLdsBytes ? (kLdsBytes - lists) / tile : 0;
+    return (int)std::max<size_t>(2, std::min<size_t>(4, fit));
+}
+
 template <bool MM, int ABL = 0>
 int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     const int ksteps = (int)(a.d / 16);
     const unsigned grid = (unsigned)(p.n_utiles * p.n_splits);
 #define LGX_SL(KS)                                                                                          \
     do {                                                                                                    \
-        const size_t shmem = 2 * (size_t)LdsGeom<KS>::TILE + (size_t)kLdsWaves * list_bytes_per_wave(a.k);     \
+        const size_t lists = (size_t)kLdsWaves * list_bytes_per_wave(a.k);                                   \
+        const int nbuf = lds_ring_buffers(LdsGeom<KS>::TILE, lists);                                         \
+        const size_t shmem = (size_t)nbuf * LdsGeom<KS>::TILE + lists;                                       \
         int rc_ = set_lds_limit(score_topk_bf16_lds<KS, MM, ABL>, shmem);                                 \
         if (rc_) return rc_;                                                                                \
-        score_topk_bf16_lds<KS, MM, ABL><<<grid, 512, shmem, stream>>>(a, p.xcd_affine ? 1 : 0, p.n_utiles); \
+        score_topk_bf16_lds<KS, MM, ABL><<<grid, 512, shmem, stream>>>(a, p.xcd_affine ? 1 : 0, p.n_utiles, \
+                                                                       nbuf);                               \
     } while (0)
     switch (ksteps) {
         case 2: LGX_SL(2); break;
@@ -891,36 +908,6 @@ int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
             return LGX_ERR_UNSUPPORTED;
     }
 #undef LGX_SL
-    LGX_LAUNCH_CHECK();
-    return LGX_OK;
-}
-
-template <bool MM, int ABL = 0>
-int launch_ring(const ScoreArgs& a, const SplitPlan& p, int* err, hipStream_t stream) {
-    const int ksteps = (int)(a.d / 16);
-    const unsigned grid = (unsigned)(p.n_utiles * p.n_splits);
-#define LGX_SR(KS)                                                                                           \
-    do {                                                                                                     \
-        const size_t shmem = (size_t)kRingSlots * RingGeom<KS>::SLOT + 2 * kRingSlots * sizeof(int) + 16 +  \
-                             (size_t)kLdsWaves * list_bytes_per_wave(a.k);                                  \
-        int rc_ = set_lds_limit(score_topk_bf16_ring<KS, MM, ABL>, shmem);                                 \
-        if (rc_) return rc_;                                                                                 \
-        score_topk_bf16_ring<KS, MM, ABL><<<grid, 512, shmem, stream>>>(a, p.xcd_affine ? 1 : 0, p.n_utiles, err); \
-    } while (0)
-    switch (ksteps) {
-        case 2: LGX_SR(2); break;
-        case 4: LGX_SR(4); break;
-        case 6: LGX_SR(6); break;
-        case 8: LGX_SR(8); break;
-        case 10: LGX_SR(10); break;
-        case 12: LGX_SR(12); break;
-        case 14: LGX_SR(14); break;
-        case 16: LGX_SR(16); break;
-        default:
-            set_error("lgx_score_topk: no ring kernel for d=%lld", (long long)a.d);
-            return LGX_ERR_UNSUPPORTED;
-    }
-#undef LGX_SR
     LGX_LAUNCH_CHECK();
     return LGX_OK;
 }
@@ -975,19 +962,13 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
     }
     const bool mm = minmax_out != nullptr;
     int rc;
-    // development switches (A/B and ablation only): LGX_SCORE_KERNEL=ring selects the decoupled
-    // ring kernel; LGX_SCORE_ABLATE=1 drops the top-k work, =3 the mask path (timing studies)
+    // development switches (timing studies only): LGX_SCORE_ABLATE=1 drops the top-k work,
+    // =3 keeps only its fast-path filter
     static const char* abl_env = getenv("LGX_SCORE_ABLATE");
     static const bool ablate = abl_env && abl_env[0] == '1';
-    static const bool ablate2 = abl_env && abl_env[0] == '2';
     static const bool ablate3 = abl_env && abl_env[0] == '3';
-    static const bool ring = getenv("LGX_SCORE_KERNEL") && getenv("LGX_SCORE_KERNEL")[0] == 'r';
-    int* err = reinterpret_cast<int*>(base + 2 * list_bytes + 256);
-    if (p.lds && ablate && ring) rc = launch_ring<false, 1>(a, p, err, stream);
-    else if (p.lds && ablate2 && ring) rc = launch_ring<false, 2>(a, p, err, stream);
-    else if (p.lds && ablate) rc = launch_lds<false, 1>(a, p, stream);
+    if (p.lds && ablate) rc = launch_lds<false, 1>(a, p, stream);
     else if (p.lds && ablate3) rc = launch_lds<false, 3>(a, p, stream);
-    else if (p.lds && ring) rc = mm ? launch_ring<true>(a, p, err, stream) : launch_ring<false>(a, p, err, stream);
     else if (p.lds) rc = mm ? launch_lds<true>(a, p, stream) : launch_lds<false>(a, p, stream);
     else if (dtype == LGX_DTYPE_F32) rc = mm ? launch_v1<LGX_DTYPE_F32, true>(a, kch, stream)
                                              : launch_v1<LGX_DTYPE_F32, false>(a, kch, stream);
