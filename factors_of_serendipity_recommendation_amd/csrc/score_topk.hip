@@ -33,14 +33,14 @@ namespace {
 // Development statistics (tools/score_stats.hip defines LGX_SCORE_STATS; the library never does):
 // per-wave counters and s_memtime cycle stamps, summed into a device array at the end.
 #ifdef LGX_SCORE_STATS
-__device__ unsigned long long g_score_stats[8];
-#define LGX_STAT_DECL uint64_t stat_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+__device__ unsigned long long g_score_stats[12];
+#define LGX_STAT_DECL uint64_t stat_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #define LGX_STAT(i, v) (stat_[i] += (v))
 #define LGX_STAT_T0 const uint64_t stat_t0_ = __builtin_amdgcn_s_memtime();
 #define LGX_STAT_T1(i) LGX_STAT(i, __builtin_amdgcn_s_memtime() - stat_t0_);
 #define LGX_STAT_FLUSH                                                                                 \
     if ((threadIdx.x & 63) == 0)                                                                       \
-        for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_score_stats[i_], (unsigned long long)stat_[i_]);
+        for (int i_ = 0; i_ < 12; ++i_) atomicAdd(&g_score_stats[i_], (unsigned long long)stat_[i_]);
 #else
 #define LGX_STAT_DECL
 #define LGX_STAT(i, v)
@@ -161,41 +161,51 @@ struct WaveTopK {
     // deferred candidates of THIS lane (its half's items), inserted into the list in batches so
     // that a late-sweep survivor costs a few register moves instead of LDS round trips
     static constexpr int kPend = kPendSlots;
+    static_assert(kPend == 4, "drop_masked's lockstep search is written for 4 slots");
     LGX_STAT_DECL
     uint64_t* pend;  // this lane's kPend slots in LDS
     int pcnt;
     float tau;       // filter threshold: -inf until the list is full, +inf for padding users
     int32_t tau_i;
     float mn, mx;
-    // 256-bit Bloom filter of the user's masked items (2 hashes), as 8 scalars so that the
-    // word select stays in registers
-    uint32_t bl0, bl1, bl2, bl3, bl4, bl5, bl6, bl7;
+    // 512-bit Bloom filter of the user's masked items (2 hashes; false-positive rate ~3% at 50
+    // masked items), as 16 scalars so that the word select stays in registers
+    uint32_t bl[16];
 
-    __device__ __forceinline__ static uint32_t bloom_h1(int32_t x) { return ((uint32_t)x * 0x9E3779B1u) >> 24; }
-    __device__ __forceinline__ static uint32_t bloom_h2(int32_t x) { return ((uint32_t)x * 0x85EBCA77u) >> 24; }
+    __device__ __forceinline__ static uint32_t bloom_h1(int32_t x) { return ((uint32_t)x * 0x9E3779B1u) >> 23; }
+    __device__ __forceinline__ static uint32_t bloom_h2(int32_t x) { return ((uint32_t)x * 0x85EBCA77u) >> 23; }
     __device__ __forceinline__ bool bloom_test(uint32_t hv) const {
         // AND with per-word masks: no select over loaded members (which the compiler would turn
         // into a load through a selected pointer and force the state into scratch)
         const uint32_t q = hv >> 5, m = 1u << (hv & 31);
-        const uint32_t hit = (bl0 & (q == 0 ? m : 0u)) | (bl1 & (q == 1 ? m : 0u)) |
-                             (bl2 & (q == 2 ? m : 0u)) | (bl3 & (q == 3 ? m : 0u)) |
-                             (bl4 & (q == 4 ? m : 0u)) | (bl5 & (q == 5 ? m : 0u)) |
-                             (bl6 & (q == 6 ? m : 0u)) | (bl7 & (q == 7 ? m : 0u));
+        uint32_t hit = 0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) hit |= bl[w] & (q == (uint32_t)w ? m : 0u);
         return hit != 0u;
     }
     __device__ __forceinline__ void bloom_set(uint32_t hv) {
         const uint32_t q = hv >> 5, m = 1u << (hv & 31);
-        bl0 |= q == 0 ? m : 0u; bl1 |= q == 1 ? m : 0u; bl2 |= q == 2 ? m : 0u; bl3 |= q == 3 ? m : 0u;
-        bl4 |= q == 4 ? m : 0u; bl5 |= q == 5 ? m : 0u; bl6 |= q == 6 ? m : 0u; bl7 |= q == 7 ? m : 0u;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) bl[w] |= q == (uint32_t)w ? m : 0u;
     }
     // exact test only when the filter cannot rule the item out
-    __device__ __forceinline__ bool masked(const ScoreArgs& a, int32_t it) const {
+    __device__ __forceinline__ bool masked(const ScoreArgs& a, int32_t it) {
         if (!a.mask_indptr) return false;
+        LGX_STAT(8, 1);
         if (!bloom_test(bloom_h1(it)) || !bloom_test(bloom_h2(it))) return false;
+        LGX_STAT(9, 1);
+#ifdef LGX_SCORE_STATS
+        const uint64_t t0_ = __builtin_amdgcn_s_memtime();
+        const bool r_ = is_masked(a, b, it);
+        stat_[10] += __builtin_amdgcn_s_memtime() - t0_;
+        return r_;
+#else
         return is_masked(a, b, it);
+#endif
     }
     __device__ __forceinline__ void build_bloom(const ScoreArgs& a) {
-        bl0 = bl1 = bl2 = bl3 = bl4 = bl5 = bl6 = bl7 = 0u;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) bl[w] = 0u;
         if (!a.mask_indptr || !user_ok) return;
         const int64_t m0 = a.mask_indptr[b], m1 = a.mask_indptr[b + 1];
         for (int64_t j = m0; j < m1; ++j) {
@@ -263,13 +273,18 @@ struct WaveTopK {
                 if (NACC == 2 && row_off(1, r) >= rem) acc1[r] = -INFINITY;
             }
         }
-        float m = acc0[0];
+        // maxima of the 8-score groups {acc0 rows 0-7, 8-15, acc1 rows 0-7, 8-15}: the fast-path
+        // test, and the event path visits only groups whose maximum reaches tau
+        float g[2 * NACC];
 #pragma unroll
-        for (int r = 1; r < 16; ++r) m = fmaxf(m, acc0[r]);
-        if (NACC == 2) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) m = fmaxf(m, acc1[r]);
+        for (int q = 0; q < 2 * NACC; ++q) {
+            const f32x16& acc = q < 2 ? acc0 : acc1;
+            const int r0 = (q & 1) * 8;
+            g[q] = fmaxf(fmaxf(fmaxf(acc[r0], acc[r0 + 1]), fmaxf(acc[r0 + 2], acc[r0 + 3])),
+                         fmaxf(fmaxf(acc[r0 + 4], acc[r0 + 5]), fmaxf(acc[r0 + 6], acc[r0 + 7])));
         }
+        float m = fmaxf(g[0], g[1]);
+        if (NACC == 2) m = fmaxf(m, fmaxf(g[2], g[3]));
         if (MINMAX && user_ok) {
             float lo = INFINITY;
 #pragma unroll
@@ -289,7 +304,7 @@ struct WaveTopK {
 #ifdef LGX_SCORE_STATS
         const uint64_t ev_t0 = __builtin_amdgcn_s_memtime();
 #endif
-        slow<NACC>(a, acc0, acc1, ib, rem);
+        slow<NACC>(a, acc0, acc1, g, ib, rem);
 #ifdef LGX_SCORE_STATS
         stat_[7] += __builtin_amdgcn_s_memtime() - ev_t0;
 #endif
@@ -298,8 +313,8 @@ struct WaveTopK {
     __device__ __forceinline__ static int32_t row_off(int j, int r) { return 32 * j + (r & 3) + 8 * (r >> 2); }
 
     template <int NACC>
-    __device__ __forceinline__ void slow(const ScoreArgs& a, const f32x16& acc0, const f32x16& acc1, int64_t ib,
-                                         int32_t rem) {
+    __device__ __forceinline__ void slow(const ScoreArgs& a, const f32x16& acc0, const f32x16& acc1, const float* g,
+                                         int64_t ib, int32_t rem) {
         if (__ballot(len < k) != 0ull) {  // a list is still filling (first block): exact inserts
             LGX_STAT(3, 1);
             drain(a);
@@ -312,9 +327,11 @@ struct WaveTopK {
         const int32_t lim = l64 > (1 << 30) ? (1 << 30) : l64 < -1 ? -1 : (int32_t)l64;
         uint32_t ovf = 0;
 #pragma unroll
-        for (int j = 0; j < NACC; ++j) {
+        for (int q = 0; q < 2 * NACC; ++q) {
+            if (__ballot(g[q] >= tau) == 0ull) continue;  // no lane has a survivor in this group
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
+            for (int rr = 0; rr < 8; ++rr) {
+                const int j = q >> 1, r = (q & 1) * 8 + rr;
                 const float sc = j ? acc1[r] : acc0[r];
                 if (sc >= tau) {
                     const int32_t off = row_off(j, r);
@@ -369,19 +386,68 @@ struct WaveTopK {
         return cmask;
     }
 
-    // one candidate into this lane's user list (the caller serialises the two lane halves)
+    // one candidate into this lane's user list (the caller serialises the two lane halves);
+    // CHECK: test the mask here (drained keys were already filtered by drop_masked)
+    template <bool CHECK>
     __device__ __forceinline__ void insert_key(const ScoreArgs& a, uint64_t key) {
         const int32_t it = key_index(key);
         if (len == k) {
-            if (key <= kmin || masked(a, it)) return;
+            if (key <= kmin || (CHECK && masked(a, it))) return;
             keys[mp] = key;
             rescan();
         } else {
-            if (masked(a, it)) return;
+            if (CHECK && masked(a, it)) return;
             keys[len++] = key;
             if (len == k) rescan();
         }
     }
+
+    // bit j of the result: pending key j is NOT masked.  The filter rules most keys out; the rest
+    // are looked up by up to kPend binary searches advanced in lockstep, so each level issues its
+    // loads together and waits once (a global load also waits for the in-flight tile DMA).
+    __device__ __forceinline__ uint32_t drop_masked(const ScoreArgs& a) {
+        uint32_t keep = (1u << pcnt) - 1u;
+        if (!a.mask_indptr) return keep;
+        int32_t it[kPend];
+        uint32_t need = 0;
+#pragma unroll
+        for (int j = 0; j < kPend; ++j) {
+            it[j] = j < pcnt ? key_index(pend[j]) : 0;
+            if (j < pcnt && bloom_test(bloom_h1(it[j])) && bloom_test(bloom_h2(it[j]))) need |= 1u << j;
+        }
+        if (__ballot(need != 0u) == 0ull) return keep;
+        LGX_STAT(9, 1);
+        const int64_t m0 = need ? a.mask_indptr[b] : 0, m1 = need ? a.mask_indptr[b + 1] : 0;
+        const int32_t* mi = a.mask_indices + m0;
+        int32_t lo[kPend], hi[kPend];
+#pragma unroll
+        for (int j = 0; j < kPend; ++j) {
+            lo[j] = 0;
+            hi[j] = (need >> j) & 1u ? (int32_t)(m1 - m0) : 0;
+        }
+        // first index with mi[idx] >= it, for every needed key at once
+        while (__ballot(((need != 0u) & ((lo[0] < hi[0]) | (lo[1] < hi[1]) | (lo[2] < hi[2]) | (lo[3] < hi[3])))) != 0ull) {
+            int32_t v[kPend];
+#pragma unroll
+            for (int j = 0; j < kPend; ++j) v[j] = lo[j] < hi[j] ? mi[(lo[j] + hi[j]) >> 1] : 0;
+#pragma unroll
+            for (int j = 0; j < kPend; ++j) {
+                if (lo[j] < hi[j]) {
+                    const int32_t mid = (lo[j] + hi[j]) >> 1;
+                    if (v[j] < it[j]) lo[j] = mid + 1;
+                    else hi[j] = mid;
+                }
+            }
+        }
+        int32_t w[kPend];
+#pragma unroll
+        for (int j = 0; j < kPend; ++j) w[j] = ((need >> j) & 1u) && lo[j] < (int32_t)(m1 - m0) ? mi[lo[j]] : -1;
+#pragma unroll
+        for (int j = 0; j < kPend; ++j)
+            if (((need >> j) & 1u) && w[j] == it[j]) keep &= ~(1u << j);
+        return keep;
+    }
+
     // after half ph changed the list: the other half adopts {len, mp, kmin} (cross-half swap)
     __device__ __forceinline__ void sync_from(int ph) {
         __builtin_amdgcn_wave_barrier();  // list writes of half ph precede the other half's reads
@@ -399,16 +465,20 @@ struct WaveTopK {
             tau_i = key_index(kmin);
         }
     }
-    // insert every deferred candidate of the wave (both halves, serialised)
+    // insert every deferred candidate of the wave: mask filter for both halves at once, then the
+    // list updates half by half
     __device__ __forceinline__ void drain(const ScoreArgs& a) {
+        if (__ballot(pcnt > 0) == 0ull) return;
+        const uint32_t keep = drop_masked(a);
         for (int ph = 0; ph < 2; ++ph) {
             if (__ballot(ph == h && pcnt > 0) == 0ull) continue;
             if (ph == h) {
-                for (int j = 0; j < pcnt; ++j) insert_key(a, pend[j]);
-                pcnt = 0;
+                for (int j = 0; j < pcnt; ++j)
+                    if ((keep >> j) & 1u) insert_key<false>(a, pend[j]);
             }
             sync_from(ph);
         }
+        pcnt = 0;
         refresh_tau();
     }
     // insert a block's survivors directly (pending list already drained)
@@ -422,7 +492,7 @@ struct WaveTopK {
                 while (todo) {  // one copy of the insertion code, one iteration per survivor
                     const int r = __builtin_ctz(todo);
                     todo &= todo - 1;
-                    insert_key(a, make_key(pick<NACC>(acc0, acc1, r), item_of(ib, r)));
+                    insert_key<true>(a, make_key(pick<NACC>(acc0, acc1, r), item_of(ib, r)));
                 }
             }
             sync_from(ph);
@@ -597,8 +667,8 @@ __global__ __launch_bounds__(512) void score_topk_bf16_lds(ScoreArgs a, int xcd_
         asm volatile("" : "+v"(t));
         uf[c] = __builtin_bit_cast(uint4, t);
     }
-    asm volatile("" : "+v"(st.bl0), "+v"(st.bl1), "+v"(st.bl2), "+v"(st.bl3), "+v"(st.bl4), "+v"(st.bl5),
-                 "+v"(st.bl6), "+v"(st.bl7));
+#pragma unroll
+    for (int w = 0; w < 16; ++w) asm volatile("" : "+v"(st.bl[w]));
 
     const int64_t i_begin = (int64_t)split * a.split_items;
     const int64_t i_end = min(a.n_items, i_begin + a.split_items);
@@ -967,7 +1037,11 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
     static const char* abl_env = getenv("LGX_SCORE_ABLATE");
     static const bool ablate = abl_env && abl_env[0] == '1';
     static const bool ablate3 = abl_env && abl_env[0] == '3';
-    if (p.lds && ablate) rc = launch_lds<false, 1>(a, p, stream);
+    static const bool ablate4 = abl_env && abl_env[0] == '4';  // kernel ignores the mask
+    ScoreArgs ka = a;
+    if (ablate4) ka.mask_indptr = nullptr;
+    if (p.lds && ablate4) rc = launch_lds<false>(ka, p, stream);
+    else if (p.lds && ablate) rc = launch_lds<false, 1>(a, p, stream);
     else if (p.lds && ablate3) rc = launch_lds<false, 3>(a, p, stream);
     else if (p.lds) rc = mm ? launch_lds<true>(a, p, stream) : launch_lds<false>(a, p, stream);
     else if (dtype == LGX_DTYPE_F32) rc = mm ? launch_v1<LGX_DTYPE_F32, true>(a, kch, stream)
