@@ -222,13 +222,33 @@ def bench_scoring(args, rank, world):
     elapsed = max_over_ranks(time.perf_counter() - t_start, world)
     mean_launch = float(np.mean([a.elapsed_time(b) for a, b in ev])) / 1e3
     flops = 2.0 * B * n_items * d
-    traffic, traffic_src = measured_traffic(args.config, world, ["score_topk_kernel"])
+    traffic, traffic_src = measured_traffic(args.config, world, ["score_topk_bf16_lds"])
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = scoring_cpu_baseline(Q, items, pos, k, args.cpu_score_users)
     return {"value": B_total * n_items * steps / elapsed, "unit": "items/s", "users_per_step": B_total,
             "n_items": n_items, "d": d, "k": k, "dtype": "bf16", "ms_per_step": elapsed / steps * 1e3,
             "roofline": {"bound": "mfma", "achieved": flops / mean_launch / 1e12, "peak": BF16_MFMA_PEAK / 1e12,
                          "unit": "TFLOP/s", "frac": flops / mean_launch / BF16_MFMA_PEAK, "traffic": traffic,
                          "traffic_unit": "GB/launch", "traffic_source": traffic_src,
-                         "kernel": "score_topk_kernel (+finalize)"}}
+                         "kernel": "score_topk_bf16_lds (+ score_topk_finalize, both inside the timed launch)"},
+            "cpu_baseline": cpu}
+
+
+def scoring_cpu_baseline(Q, items, pos, k, n_users):
+    """The reference's CPU scoring procedure (Procedure.py:121-135 per 100-user batch: fp32 matmul,
+    sigmoid, train mask, torch.topk) on the first n_users query users of the same batch."""
+    from oracle import torch_ref
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    Qc = Q[:n_users].float().cpu()
+    Ic = items.float().cpu()
+    masks = [row for row in pos[:n_users].cpu().numpy()]
+    torch_ref.score_topk_cpu(Qc[:100], Ic, k, masks[:100])  # warm-up
+    _, t = torch_ref.score_topk_cpu(Qc, Ic, k, masks)
+    return {"value": n_users * items.shape[0] / t, "unit": "items/s", "cores": threads, "kind": "port",
+            "sample": f"{n_users} of the query users x {items.shape[0]} items, d={items.shape[1]} fp32, "
+                      f"top-{k} with the same train masks ({t:.1f}s)"}
 
 
 def main():
@@ -242,6 +262,7 @@ def main():
     ap.add_argument("--score-items", type=int, default=1_000_000)
     ap.add_argument("--score-steps", type=int, default=2)
     ap.add_argument("--cpu-nnz", type=int, default=6_000_000)
+    ap.add_argument("--cpu-score-users", type=int, default=2000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scoring", action="store_true")
     ap.add_argument("--no-propagation", action="store_true", help="development: scoring leg only")

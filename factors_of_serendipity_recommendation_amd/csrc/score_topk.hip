@@ -111,10 +111,6 @@ struct ScoreArgs {
     uint32_t* minmax;     // ordered {min, max} or nullptr
 };
 
-__device__ __forceinline__ bool better(float s1, int32_t i1, float s2, int32_t i2) {
-    return s1 > s2 || (s1 == s2 && i1 < i2);
-}
-
 __device__ __forceinline__ bool is_masked(const ScoreArgs& a, int64_t b, int32_t item) {
     if (!a.mask_indptr) return false;
     int64_t lo = a.mask_indptr[b], hi = a.mask_indptr[b + 1];
@@ -597,10 +593,15 @@ struct LdsGeom {
 // the tiles of the LDS ring apart and would put an s_waitcnt vmcnt(0) in front of every later LDS
 // read, which serialises the prefetch.  The kernel orders the DMA itself: counted vmcnt (this
 // wave's pieces) + workgroup barrier (everyone's), as the hardware requires.
+// M0 is a reserved register: clang accepts but ignores the clobber (-Winline-asm).  That is safe
+// here because nothing else in this file uses M0 (the generated code's only M0 writes are these).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ void lds_dma16(const void* sbase, uint32_t voff, uint32_t lds_addr) {
     asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
                  :: "v"(voff), "s"(sbase), "s"(lds_addr) : "memory", "m0");
 }
+#pragma clang diagnostic pop
 
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n (conservative above 15)
 __device__ __forceinline__ void wait_vmcnt_le(int n) {
@@ -982,9 +983,40 @@ int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     return LGX_OK;
 }
 
-size_t topk_ws_bytes(int64_t B, int64_t n_items, int k, int dtype, int64_t d) {
+// A batch runs as up to two launches over user ranges.  The LDS kernel's full-sweep mode runs
+// one workgroup per CU per round; when the last round would leave most CUs idle, the users of that
+// partial round become a second launch whose catalog splits fill the chip.
+constexpr int64_t kRoundTiles = 256;  // workgroups resident at once (one per CU)
+struct UserRange {
+    int64_t u0, u1;
+    SplitPlan p;
+    size_t ws_off;  // partial lists of this range inside the workspace
+};
+
+int plan_ranges(int64_t B, int64_t n_items, int dtype, int64_t d, int k, UserRange* r) {
     const SplitPlan p = plan_splits(B, n_items, dtype, d, k);
-    return align_up((size_t)B * p.n_splits * k * 4) * 2 + 512;
+    int n = 0;
+    int64_t full = B;
+    if (p.lds && p.n_splits == 1 && p.n_utiles >= 2 * kRoundTiles) {  // full-sweep mode
+        const int64_t rem_tiles = p.n_utiles % kRoundTiles;
+        if (rem_tiles != 0 && rem_tiles < kRoundTiles * 3 / 4) full = (p.n_utiles - rem_tiles) * kLdsUsers;
+    }
+    size_t off = 0;
+    r[n++] = {0, full, plan_splits(full, n_items, dtype, d, k), 0};
+    if (full < B) r[n++] = {full, B, plan_splits(B - full, n_items, dtype, d, k), 0};
+    for (int i = 0; i < n; ++i) {
+        r[i].ws_off = off;
+        off += align_up((size_t)(r[i].u1 - r[i].u0) * r[i].p.n_splits * k * 4) * 2;
+    }
+    return n;
+}
+
+size_t topk_ws_bytes(int64_t B, int64_t n_items, int k, int dtype, int64_t d) {
+    UserRange r[2];
+    const int n = plan_ranges(B, n_items, dtype, d, k, r);
+    size_t bytes = 0;
+    for (int i = 0; i < n; ++i) bytes += align_up((size_t)(r[i].u1 - r[i].u0) * r[i].p.n_splits * k * 4) * 2;
+    return bytes + 512;  // + the global min / max words
 }
 
 }  // namespace
@@ -1020,36 +1052,50 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
                 "lgx_score_topk: empty or oversized catalog");
     const size_t need = topk_ws_bytes(B, n_items, k, dtype, d);
     LGX_REQUIRE(ws && ws_bytes >= need, LGX_ERR_WORKSPACE, "lgx_score_topk: workspace %zu < %zu", ws_bytes, need);
-    const SplitPlan p = plan_splits(B, n_items, dtype, d, k);
+    UserRange ranges[2];
+    const int n_ranges = plan_ranges(B, n_items, dtype, d, k, ranges);
     char* base = static_cast<char*>(ws);
-    const size_t list_bytes = align_up((size_t)B * p.n_splits * k * 4);
-    ScoreArgs a{Q, user_rows, items, B, n_items, d, mask_indptr, mask_indices, k, p.n_splits, p.split_items,
-                reinterpret_cast<float*>(base), reinterpret_cast<int32_t*>(base + list_bytes),
-                minmax_out ? reinterpret_cast<uint32_t*>(base + 2 * list_bytes) : nullptr};
-    if (a.minmax) {
-        minmax_init<<<1, 1, 0, stream>>>(a.minmax);
+    uint32_t* minmax = minmax_out ? reinterpret_cast<uint32_t*>(base + need - 512) : nullptr;
+    if (minmax) {
+        minmax_init<<<1, 1, 0, stream>>>(minmax);
         LGX_LAUNCH_CHECK();
     }
     const bool mm = minmax_out != nullptr;
-    int rc;
     // development switches (timing studies only): LGX_SCORE_ABLATE=1 drops the top-k work,
-    // =3 keeps only its fast-path filter
+    // =3 keeps only its fast-path filter, =4 hides the mask from the scoring kernel
     static const char* abl_env = getenv("LGX_SCORE_ABLATE");
     static const bool ablate = abl_env && abl_env[0] == '1';
     static const bool ablate3 = abl_env && abl_env[0] == '3';
-    static const bool ablate4 = abl_env && abl_env[0] == '4';  // kernel ignores the mask
-    ScoreArgs ka = a;
-    if (ablate4) ka.mask_indptr = nullptr;
-    if (p.lds && ablate4) rc = launch_lds<false>(ka, p, stream);
-    else if (p.lds && ablate) rc = launch_lds<false, 1>(a, p, stream);
-    else if (p.lds && ablate3) rc = launch_lds<false, 3>(a, p, stream);
-    else if (p.lds) rc = mm ? launch_lds<true>(a, p, stream) : launch_lds<false>(a, p, stream);
-    else if (dtype == LGX_DTYPE_F32) rc = mm ? launch_v1<LGX_DTYPE_F32, true>(a, kch, stream)
-                                             : launch_v1<LGX_DTYPE_F32, false>(a, kch, stream);
-    else rc = mm ? launch_v1<LGX_DTYPE_BF16, true>(a, kch, stream) : launch_v1<LGX_DTYPE_BF16, false>(a, kch, stream);
-    if (rc) return rc;
-    score_topk_finalize<<<(unsigned)a.B, 64, 0, stream>>>(a, mask_value, apply_sigmoid, out_idx, out_val, minmax_out);
-    LGX_LAUNCH_CHECK();
+    static const bool ablate4 = abl_env && abl_env[0] == '4';
+    const size_t esz = dtype == LGX_DTYPE_F32 ? 4 : 2;
+    for (int i = 0; i < n_ranges; ++i) {
+        const UserRange& R = ranges[i];
+        const SplitPlan& p = R.p;
+        const int64_t Bi = R.u1 - R.u0;
+        const size_t list_bytes = align_up((size_t)Bi * p.n_splits * k * 4);
+        char* wsr = base + R.ws_off;
+        const void* Qi = user_rows ? Q : static_cast<const void*>(static_cast<const char*>(Q) + R.u0 * d * esz);
+        ScoreArgs a{Qi, user_rows ? user_rows + R.u0 : nullptr, items, Bi, n_items, d,
+                    mask_indptr ? mask_indptr + R.u0 : nullptr, mask_indices, k, p.n_splits, p.split_items,
+                    reinterpret_cast<float*>(wsr), reinterpret_cast<int32_t*>(wsr + list_bytes), minmax};
+        int rc;
+        ScoreArgs ka = a;
+        if (ablate4) ka.mask_indptr = nullptr;
+        if (p.lds && ablate4) rc = launch_lds<false>(ka, p, stream);
+        else if (p.lds && ablate) rc = launch_lds<false, 1>(a, p, stream);
+        else if (p.lds && ablate3) rc = launch_lds<false, 3>(a, p, stream);
+        else if (p.lds) rc = mm ? launch_lds<true>(a, p, stream) : launch_lds<false>(a, p, stream);
+        else if (dtype == LGX_DTYPE_F32) rc = mm ? launch_v1<LGX_DTYPE_F32, true>(a, kch, stream)
+                                                 : launch_v1<LGX_DTYPE_F32, false>(a, kch, stream);
+        else rc = mm ? launch_v1<LGX_DTYPE_BF16, true>(a, kch, stream)
+                     : launch_v1<LGX_DTYPE_BF16, false>(a, kch, stream);
+        if (rc) return rc;
+        // min / max is final after the last range's kernel (stream order): only its finalize reports it
+        score_topk_finalize<<<(unsigned)Bi, 64, 0, stream>>>(a, mask_value, apply_sigmoid, out_idx + R.u0 * k,
+                                                             out_val ? out_val + R.u0 * k : nullptr,
+                                                             i + 1 == n_ranges ? minmax_out : nullptr);
+        LGX_LAUNCH_CHECK();
+    }
     return LGX_OK;
 }
 

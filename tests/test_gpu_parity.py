@@ -273,10 +273,26 @@ def test_score_topk_bf16_masked_minmax(d, k):
     assert np.allclose(mm.cpu().numpy(), [Sf.min(), Sf.max()], rtol=1e-5, atol=1e-5)
 
 
+def test_score_topk_bf16_tiny_catalog_many_users():
+    """A catalog of one tile with > 256 user tiles' worth of users (single split, no tail launch)."""
+    rng = np.random.default_rng(77)
+    B, I, d, k = 70000, 40, 64, 20
+    Q = _bf16_round(rng.standard_normal((B, d)).astype(np.float32))
+    items = _bf16_round(rng.standard_normal((I, d)).astype(np.float32))
+    masks = [np.unique(rng.integers(0, I, 5)) for _ in range(B)]
+    mask = ops.lists_to_device_csr(masks, DEV)
+    idx, _ = lgx.score_topk(torch.from_numpy(Q).to(DEV).bfloat16(), torch.from_numpy(items).to(DEV).bfloat16(), k,
+                            mask=mask)
+    idx = idx.cpu().numpy()
+    sel = np.random.default_rng(1).choice(B, 500, replace=False)
+    assert_topk_sets(idx[sel], _oracle_scores(Q[sel], items, [masks[i] for i in sel]), k, 1e-5)
+
+
 def test_score_topk_bf16_full_sweep_many_users():
     """>= 512 user tiles: one catalog split, every workgroup sweeps the whole catalog from an
-    XCD-dependent rotation (tail tile included).  Checked on the device against float64 scores:
-    k distinct unmasked items per user, each within tolerance of the exact k-th best."""
+    XCD-dependent rotation (tail tile included); 513 tiles also split off the last partial round as
+    a second, catalog-split launch.  Checked on the device against float64 scores: k distinct
+    unmasked items per user, each within tolerance of the exact k-th best; global min / max."""
     g = torch.Generator(device=DEV).manual_seed(7)
     B, I, d, k = 131072 + 77, 1000 + 13, 64, 20
     Q = (torch.randn(B, d, device=DEV, generator=g) * 0.5).bfloat16()
@@ -288,8 +304,10 @@ def test_score_topk_bf16_full_sweep_many_users():
     indptr = torch.zeros(B + 1, dtype=torch.int64, device=DEV)
     indptr[1:] = torch.cumsum(lens, 0)
     mask = (indptr, m[keep].to(torch.int32))
-    idx, val = lgx.score_topk(Q, items, k, mask=mask)
+    idx, val, mm = lgx.score_topk(Q, items, k, mask=mask, want_minmax=True)
     S = Q.double() @ items.double().T
+    mm_ref = torch.stack([S.min(), S.max()]).cpu().numpy()
+    assert np.allclose(mm.cpu().numpy(), mm_ref, rtol=1e-5, atol=1e-5)
     rows = torch.repeat_interleave(torch.arange(B, device=DEV), lens)
     S[rows, mask[1].long()] = float("-inf")
     kth = torch.topk(S, k, dim=1).values[:, -1:]

@@ -1,0 +1,82 @@
+"""Summarise tools/profile_round.sh output (gpurun_out/prof_<tag>/) into profiles/<tag>_<config>_*:
+kernel stats, the raw PMC rows of our kernels, and per-launch HBM traffic
+(2 * FETCH_SIZE + WRITE_SIZE, KB -> bytes; the x2 is the gfx950 correction for 16-B/lane reads in
+MI355X_MICROARCH.md).  Usage: python tools/pmc_summary.py r01 [--config synth10m] [--src DIR] [--dst DIR]"""
+import csv
+import glob
+import json
+import os
+import re
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name: str) -> str:
+    m = re.search(r"::(\w+)<", name) or re.search(r"(\w+)\(", name)
+    return m.group(1) if m else name
+
+
+def pmc_rows(path_glob, counter):
+    rows = []
+    for f in glob.glob(path_glob, recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if r.get("Counter_Name") == counter and "lgx::" in r.get("Kernel_Name", ""):
+                    rows.append(r)
+    return rows
+
+
+def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("--config", default="synth10m")
+    ap.add_argument("--src", default=None, help="default gpurun_out/prof_<tag>")
+    ap.add_argument("--dst", default=os.path.join(ROOT, "profiles"))
+    args = ap.parse_args()
+    tag, config = args.tag, args.config
+    src = args.src or os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = args.dst
+    os.makedirs(dst, exist_ok=True)
+    pre = os.path.join(dst, f"{tag}_{config}_")
+    stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], pre + "kernel_stats.csv")
+    for name in ("bench.json", "bench_under_rocprof.json"):
+        if os.path.exists(os.path.join(src, name)):
+            shutil.copy(os.path.join(src, name), pre + name.replace("bench.json", "bench_line.json")
+                        if name == "bench.json" else pre + name)
+    per = defaultdict(lambda: {"FETCH_SIZE": [], "WRITE_SIZE": []})
+    for counter, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+        rows = pmc_rows(os.path.join(src, sub, "**", "*counter_collection.csv"), counter)
+        with open(pre + f"pmc_{counter.lower()}.csv", "w", newline="") as fh:
+            if rows:
+                w = csv.DictWriter(fh, fieldnames=list(rows[0].keys()))
+                w.writeheader()
+                w.writerows(rows)
+        for r in rows:
+            per[short(r["Kernel_Name"])][counter].append(float(r["Counter_Value"]))
+    kernels = {}
+    for k, v in per.items():
+        if not v["FETCH_SIZE"] or not v["WRITE_SIZE"]:
+            continue
+        f = sum(v["FETCH_SIZE"]) / len(v["FETCH_SIZE"])
+        w = sum(v["WRITE_SIZE"]) / len(v["WRITE_SIZE"])
+        kernels[k] = {"FETCH_SIZE_KB_mean": f, "WRITE_SIZE_KB_mean": w, "dispatches": len(v["FETCH_SIZE"]),
+                      "hbm_bytes_per_launch": (2 * f + w) * 1024}
+    doc = {"workload": f"{config} (bench.py default: propagation K=3 d=128 bf16 + scoring d=256 bf16, 1M items), "
+                       "n_gpus=1",
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (tools/profile_round.sh); "
+                     "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024, the x2 being the gfx950 FETCH_SIZE "
+                     "correction for 16-B/lane reads",
+           "kernels": kernels}
+    with open(pre + "pmc_traffic.json", "w") as fh:
+        json.dump(doc, fh, indent=1)
+    print(json.dumps(doc, indent=1))
+
+
+if __name__ == "__main__":
+    main()
