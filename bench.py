@@ -79,8 +79,9 @@ def measured_traffic(config: str, world: int, kernels) -> tuple:
     return b / 1e9, os.path.relpath(files[-1], ROOT)
 
 
-def layer_bytes(nnz: int, rows: int, d: int, s: int) -> int:
-    return nnz * (4 + 4 + d * s) + rows * d * s + 8 * (rows + 1)
+def layer_bytes(nnz: int, rows: int, d: int, s: int, out_s: int = 0) -> int:
+    """col id + value + one gathered row per nonzero, one output row per row, indptr."""
+    return nnz * (4 + 4 + d * s) + rows * d * (out_s or s) + 8 * (rows + 1)
 
 
 def bench_propagation(args, rank, world):
@@ -121,7 +122,7 @@ def bench_propagation(args, rank, world):
         torch.cuda.empty_cache()
         prop = ShardedPropagation(shard, E0[:cfg.n_users], E0[cfg.n_users:], K)
         del E0
-        local_nnz = shard.A_ui.nnz + shard.A_iu.nnz
+        local_nnz = shard.A_pull.nnz + shard.A_push.nnz  # every edge of the rank's users, both directions
         local_rows = shard.n_u_local + shard.n_i_local
 
         def layer_fn(Aop, X, mode, **kw):
@@ -131,7 +132,9 @@ def bench_propagation(args, rank, world):
             ops.propagate_layer(Aop, X, mode, **kw)
             if step.record:
                 e1.record()
-                timings.append((e0, e1, layer_bytes(Aop.nnz, Aop.n_rows, d, es)))
+                # the push launch writes fp32 partial sums
+                out_s = 4 if mode == _lib.LGX_LAYER_PARTIAL else es
+                timings.append((e0, e1, layer_bytes(Aop.nnz, Aop.n_rows, d, es, out_s)))
 
         prop.layer_fn = layer_fn
 
@@ -271,9 +274,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_rank %= max(1, torch.cuda.device_count())  # identity on a real node; rehearsal ranks share a GPU
     torch.cuda.set_device(local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # LGX_BENCH_BACKEND=gloo: rehearsal of the N>1 path with ranks sharing one GPU (RCCL refuses
+        # that); measurements are always taken over RCCL ("nccl")
+        backend = os.environ.get("LGX_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
     if world != args.gpus:
         log(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}")
 

@@ -128,6 +128,12 @@ __device__ __forceinline__ void finish_chunk(const LayerArgs& a, int64_t row, in
             }
             break;
         }
+        case LGX_LAYER_PARTIAL: {
+#pragma unroll
+            for (int j = 0; j < VEC; j += 4)
+                *reinterpret_cast<float4*>(a.out + o + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+            break;
+        }
         default: {  // LGX_LAYER_ONLY
             float e[VEC];
             Vec<T>::load(static_cast<const T*>(a.E0) + o, e);
@@ -302,12 +308,12 @@ extern "C" int lgx_propagate_layer(const lgx_csr* A, const void* X, void* Y, con
                                    float n_mean, lgx_stream_t stream) {
     int rc = check_csr(A, d, dtype);
     if (rc) return rc;
-    LGX_REQUIRE(mode >= LGX_LAYER_PLAIN && mode <= LGX_LAYER_ONLY, LGX_ERR_INVALID_ARG,
+    LGX_REQUIRE(mode >= LGX_LAYER_PLAIN && mode <= LGX_LAYER_PARTIAL, LGX_ERR_INVALID_ARG,
                 "lgx_propagate_layer: bad mode %d", mode);
     LGX_REQUIRE(X || A->nnz == 0, LGX_ERR_INVALID_ARG, "lgx_propagate_layer: X is null");
     const bool needY = mode <= LGX_LAYER_MID, needE0 = mode == LGX_LAYER_FIRST || mode == LGX_LAYER_ONLY;
     const bool needAcc = mode >= LGX_LAYER_FIRST && mode <= LGX_LAYER_LAST;
-    const bool needOut = mode >= LGX_LAYER_LAST;
+    const bool needOut = mode >= LGX_LAYER_LAST;  // LAST, ONLY, PARTIAL
     LGX_REQUIRE((!needY || Y) && (!needE0 || E0) && (!needAcc || acc) && (!needOut || out),
                 LGX_ERR_INVALID_ARG, "lgx_propagate_layer: missing buffer for mode %d", mode);
     LGX_REQUIRE(!needOut || n_mean > 0.0f, LGX_ERR_INVALID_ARG, "lgx_propagate_layer: n_mean <= 0");
@@ -317,6 +323,59 @@ extern "C" int lgx_propagate_layer(const lgx_csr* A, const void* X, void* Y, con
                 X, Y, E0, acc, out, d, mode, n_mean};
     if (dtype == LGX_DTYPE_F32) return dispatch_layer<float>(a, as_hip(stream));
     return dispatch_layer<uint16_t>(a, as_hip(stream));
+}
+
+namespace lgx {
+namespace {
+// one thread per 16-B output chunk: the fused path's finish_chunk on precomputed row sums
+template <typename T>
+__global__ __launch_bounds__(kThreads) void layer_epilogue_kernel(LayerArgs a, const float* __restrict__ y,
+                                                                  int64_t rows) {
+    constexpr int VEC = Vec<T>::N;
+    const int64_t cpr = a.d / VEC;
+    const int64_t c = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (c >= rows * cpr) return;
+    const int64_t row = c / cpr, off = (c % cpr) * VEC;
+    float v[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; j += 4) {
+        const float4 q = *reinterpret_cast<const float4*>(y + row * a.d + off + j);
+        v[j] = q.x; v[j + 1] = q.y; v[j + 2] = q.z; v[j + 3] = q.w;
+    }
+    finish_chunk<T>(a, row, off, v);
+}
+}  // namespace
+}  // namespace lgx
+
+extern "C" int lgx_layer_epilogue(const float* y, int64_t rows, void* Y, const void* E0, float* acc, float* out,
+                                  int64_t d, int dtype, int mode, float n_mean, lgx_stream_t stream) {
+    LGX_REQUIRE(rows >= 0 && d > 0 && (rows == 0 || y), LGX_ERR_INVALID_ARG, "lgx_layer_epilogue: bad arguments");
+    LGX_REQUIRE(dtype == LGX_DTYPE_F32 || dtype == LGX_DTYPE_BF16, LGX_ERR_INVALID_ARG, "lgx_layer_epilogue: dtype");
+    LGX_REQUIRE(mode >= LGX_LAYER_PLAIN && mode <= LGX_LAYER_ONLY, LGX_ERR_INVALID_ARG,
+                "lgx_layer_epilogue: bad mode %d", mode);
+    const int vec = dtype == LGX_DTYPE_F32 ? 4 : 8;
+    LGX_REQUIRE(d % vec == 0, LGX_ERR_UNSUPPORTED, "lgx_layer_epilogue: d=%lld must be a multiple of %d",
+                (long long)d, vec);
+    const bool needY = mode <= LGX_LAYER_MID, needE0 = mode == LGX_LAYER_FIRST || mode == LGX_LAYER_ONLY;
+    const bool needAcc = mode >= LGX_LAYER_FIRST && mode <= LGX_LAYER_LAST, needOut = mode >= LGX_LAYER_LAST;
+    LGX_REQUIRE((!needY || Y) && (!needE0 || E0) && (!needAcc || acc) && (!needOut || out),
+                LGX_ERR_INVALID_ARG, "lgx_layer_epilogue: missing buffer for mode %d", mode);
+    LGX_REQUIRE(!needOut || n_mean > 0.0f, LGX_ERR_INVALID_ARG, "lgx_layer_epilogue: n_mean <= 0");
+    if (rows == 0) return LGX_OK;
+    LayerArgs a{};
+    a.Y = Y;
+    a.E0 = E0;
+    a.acc = acc;
+    a.out = out;
+    a.d = d;
+    a.mode = mode;
+    a.n_mean = n_mean;
+    const int64_t chunks = rows * (d / vec);
+    const unsigned grid = (unsigned)ceil_div(chunks, (int64_t)kThreads);
+    if (dtype == LGX_DTYPE_F32) layer_epilogue_kernel<float><<<grid, kThreads, 0, as_hip(stream)>>>(a, y, rows);
+    else layer_epilogue_kernel<uint16_t><<<grid, kThreads, 0, as_hip(stream)>>>(a, y, rows);
+    LGX_LAUNCH_CHECK();
+    return LGX_OK;
 }
 
 extern "C" int lgx_spmm_csr(const lgx_csr* A, const void* X, void* Y, int64_t d, int dtype,

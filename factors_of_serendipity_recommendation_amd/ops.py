@@ -42,6 +42,23 @@ def propagate_layer(A: CSRGraph, X: torch.Tensor, mode: int, Y: Optional[torch.T
                "lgx_propagate_layer")
 
 
+def layer_epilogue(y: torch.Tensor, mode: int, Y: Optional[torch.Tensor] = None, E0: Optional[torch.Tensor] = None,
+                   acc: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, n_mean: float = 1.0,
+                   dtype: Optional[torch.dtype] = None) -> None:
+    """``lgx_layer_epilogue``: the layer epilogue of ``propagate_layer`` applied to precomputed fp32
+    row sums ``y`` [rows, d] (the cross-rank sum of PARTIAL outputs).  ``dtype`` is the storage
+    type of Y / E0 (default: Y's, else E0's, else float32)."""
+    require_gpu(y)
+    if y.dtype != torch.float32 or not y.is_contiguous():
+        raise ValueError("y must be a contiguous float32 tensor")
+    ref = Y if Y is not None else E0
+    dt = dtype or (ref.dtype if ref is not None else torch.float32)
+    code = _lib.LGX_DTYPE_BF16 if dt == torch.bfloat16 else _lib.LGX_DTYPE_F32
+    _lib.check(_lib.lib().lgx_layer_epilogue(_ptr(y), y.shape[0], _ptr(Y), _ptr(E0), _ptr(acc), _ptr(out),
+                                             y.shape[1], code, mode, float(n_mean), _stream_ptr(y.device)),
+               "lgx_layer_epilogue")
+
+
 def spmm(A: CSRGraph, X: torch.Tensor) -> torch.Tensor:
     """Y = A X (the reference's ``torch.sparse.mm(G, all_emb)``, model.py:171)."""
     require_gpu(X)

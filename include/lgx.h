@@ -53,6 +53,8 @@ typedef struct ihipStream_t* lgx_stream_t; /* == hipStream_t */
 #define LGX_LAYER_MID 2   /* Y = A X ; acc += Y                                          */
 #define LGX_LAYER_LAST 3  /* out = (acc + A X) / n_mean          (Y not written)         */
 #define LGX_LAYER_ONLY 4  /* out = (E0 + A X) / n_mean           (K == 1, Y not written) */
+#define LGX_LAYER_PARTIAL 5 /* out = A X in fp32, nothing else (a rank's partial sums of a
+                               row-sharded push, reduced across ranks before the epilogue)   */
 
 /*
  * A row-partitioned CSR operator plus its launch plan.
@@ -124,6 +126,13 @@ int lgx_csr_from_coo_rows(const int64_t* coo_rows, int64_t nnz, int64_t n_rows, 
 int lgx_propagate_layer(const lgx_csr* A, const void* X, void* Y, const void* E0, float* acc,
                         float* out, int64_t d, int dtype, int mode, float n_mean,
                         lgx_stream_t stream);
+/*
+ * The epilogue of lgx_propagate_layer alone, on precomputed fp32 row sums y [rows, d] (e.g. the
+ * cross-rank sum of LGX_LAYER_PARTIAL outputs): the same per-element arithmetic as the fused path
+ * for modes PLAIN..ONLY (Y / E0 / acc / out in the layouts of lgx_propagate_layer).
+ */
+int lgx_layer_epilogue(const float* y, int64_t rows, void* Y, const void* E0, float* acc, float* out,
+                       int64_t d, int dtype, int mode, float n_mean, lgx_stream_t stream);
 /* Y = A X (alias of lgx_propagate_layer with LGX_LAYER_PLAIN). */
 int lgx_spmm_csr(const lgx_csr* A, const void* X, void* Y, int64_t d, int dtype, lgx_stream_t stream);
 /* Workspace bytes of lgx_propagate: 2 x [N,d] dtype ping-pong tables + [N,d] f32 layer sum. */

@@ -1,7 +1,7 @@
-"""CPU: the N>1 propagation schedule (row shards + per-layer all-gather, two interleaved chains)
-over a gloo process group, world sizes 2 and 3, against the float64 oracle.  The SpMM callable
-is the oracle (injected); the orchestration, padding, remapping and collectives are the product
-code of distributed.py."""
+"""CPU: the N>1 propagation schedule (user shards; items by push + reduce-scatter, users by pull
+from the all-gathered item table) over a gloo process group, world sizes 2 and 3, against the
+float64 oracle.  The SpMM and epilogue callables are the oracle (injected); the orchestration,
+operators, padding and collectives are the product code of distributed.py."""
 import os
 import socket
 
@@ -20,6 +20,13 @@ from oracle import oracle
 def cpu_layer(A, X, mode, Y=None, E0=None, acc=None, out=None, n_mean=1.0):
     y = torch.from_numpy(oracle.spmm(A.indptr.numpy(), A.indices.numpy(), A.vals.numpy(),
                                      X.float().numpy())).float()
+    if mode == _lib.LGX_LAYER_PARTIAL:
+        out.copy_(y)
+        return
+    cpu_epilogue(y, mode, Y=Y, E0=E0, acc=acc, out=out, n_mean=n_mean)
+
+
+def cpu_epilogue(y, mode, Y=None, E0=None, acc=None, out=None, n_mean=1.0):
     if mode in (_lib.LGX_LAYER_PLAIN, _lib.LGX_LAYER_FIRST, _lib.LGX_LAYER_MID):
         Y.copy_(y)
     if mode == _lib.LGX_LAYER_FIRST:
@@ -53,7 +60,7 @@ def _worker(rank, world, port, K, result_q):
         A = CSRGraph(torch.from_numpy(ip), torch.from_numpy(ix), torch.from_numpy(iv), U + I, U + I, U, I)
         E0 = torch.from_numpy((rng.standard_normal((U + I, 8)) * 0.1).astype(np.float32))
         shard = make_shard(A, U, I, rank, world, seg_len=16)
-        prop = ShardedPropagation(shard, E0[:U], E0[U:], K, layer_fn=cpu_layer)
+        prop = ShardedPropagation(shard, E0[:U], E0[U:], K, layer_fn=cpu_layer, epilogue_fn=cpu_epilogue)
         prop.step()
         prop.step()  # a second step must give the same answer (buffers re-used)
         ou, oi = prop.gather_outputs()
@@ -78,4 +85,4 @@ def test_sharded_propagation_gloo(world, K):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert eu < 1e-5 and ei < 1e-5, (eu, ei)
-    assert len(sched) == 2 * K
+    assert len(sched) == 3 * K

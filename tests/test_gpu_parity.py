@@ -18,7 +18,7 @@ import torch
 from oracle import oracle
 
 import factors_of_serendipity_recommendation_amd as lgx
-from factors_of_serendipity_recommendation_amd import evaluator, ops
+from factors_of_serendipity_recommendation_amd import _lib, evaluator, ops
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -179,6 +179,32 @@ def test_layer_modes_compose(mlls):
     assert torch.equal(out, lgx.propagate(A, E0, 3))
     ops.propagate_layer(A, E0, 4, E0=E0, out=out, n_mean=2.0)
     assert torch.equal(out, lgx.propagate(A, E0, 1))
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_partial_plus_epilogue_equals_fused_layer(mlls, dt):
+    """PARTIAL (fp32 A X) followed by lgx_layer_epilogue == the fused layer, bit for bit, in every
+    mode: the sharded propagation's item path against the single-GPU path."""
+    U, I = int(mlls["n_users"]), int(mlls["n_items"])
+    A = lgx.build_norm_adj(mlls["train_users"], mlls["train_items"], U, I, dedup=True, device=DEV)
+    E0 = torch.from_numpy(np.concatenate([mlls["emb_user"], mlls["emb_item"]])).to(DEV).to(dt)
+    N, d = E0.shape
+    y = torch.empty((N, d), dtype=torch.float32, device=DEV)
+    ops.propagate_layer(A, E0, _lib.LGX_LAYER_PARTIAL, out=y)
+    acc0 = torch.randn((N, d), device=DEV)
+    for mode in (_lib.LGX_LAYER_PLAIN, _lib.LGX_LAYER_FIRST, _lib.LGX_LAYER_MID, _lib.LGX_LAYER_LAST,
+                 _lib.LGX_LAYER_ONLY):
+        bufs = []
+        for split in (False, True):
+            Y = torch.zeros_like(E0)
+            acc, out = acc0.clone(), torch.zeros((N, d), device=DEV)
+            if split:
+                ops.layer_epilogue(y, mode, Y=Y, E0=E0, acc=acc, out=out, n_mean=3.0, dtype=dt)
+            else:
+                ops.propagate_layer(A, E0, mode, Y=Y, E0=E0, acc=acc, out=out, n_mean=3.0)
+            bufs.append((Y, acc, out))
+        for a, b in zip(*bufs):
+            assert torch.equal(a, b), mode
 
 
 # ------------------------------------------------------------------------------------ a6-a9

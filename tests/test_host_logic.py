@@ -69,21 +69,34 @@ def _cpu_graph(U, I, E, seed):
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
-def test_make_shard_remaps_columns_into_padded_tables(world):
+def test_make_shard_pull_and_push_operators(world):
+    """Pull rows reproduce the rank's user rows of A X; the push operators' partial sums, added over
+    ranks, reproduce every item row; the push operator is the exact transpose (same values)."""
     U, I = 70, 50
     A, (ip, ix, iv) = _cpu_graph(U, I, 900, world)
     X = torch.from_numpy(np.random.default_rng(0).standard_normal((U + I, 4)).astype(np.float32))
     full = oracle.spmm(ip, ix, iv, X.numpy())
+    item_sum = None
     for rank in range(world):
         s = make_shard(A, U, I, rank, world, seg_len=8)
         Xi = pad_table(X[U:], s.item_bounds, s.mi)
-        Xu = pad_table(X[:U], s.user_bounds, s.mu)
-        yu = oracle.spmm(s.A_ui.indptr.numpy(), s.A_ui.indices.numpy(), s.A_ui.vals.numpy(), Xi.numpy())
-        yi = oracle.spmm(s.A_iu.indptr.numpy(), s.A_iu.indices.numpy(), s.A_iu.vals.numpy(), Xu.numpy())
+        yu = oracle.spmm(s.A_pull.indptr.numpy(), s.A_pull.indices.numpy(), s.A_pull.vals.numpy(), Xi.numpy())
         u0, u1 = s.user_bounds[rank], s.user_bounds[rank + 1]
-        i0, i1 = s.item_bounds[rank], s.item_bounds[rank + 1]
         assert np.allclose(yu, full[u0:u1])
-        assert np.allclose(yi, full[U + i0:U + i1])
+        P = oracle.spmm(s.A_push.indptr.numpy(), s.A_push.indices.numpy(), s.A_push.vals.numpy(),
+                        X[u0:u1].numpy())
+        assert P.shape == (world * s.mi, 4)
+        item_sum = P if item_sum is None else item_sum + P
+        dense_pull = np.zeros((s.n_u_local, world * s.mi), np.float32)
+        rows = np.repeat(np.arange(s.n_u_local), np.diff(s.A_pull.indptr.numpy()))
+        dense_pull[rows, s.A_pull.indices.numpy()] = s.A_pull.vals.numpy()
+        dense_push = np.zeros((world * s.mi, s.n_u_local), np.float32)
+        rows = np.repeat(np.arange(world * s.mi), np.diff(s.A_push.indptr.numpy()))
+        dense_push[rows, s.A_push.indices.numpy()] = s.A_push.vals.numpy()
+        assert np.array_equal(dense_push, dense_pull.T)
+        assert np.all(np.diff(s.item_bounds) <= s.mi)
+    assert np.allclose(item_sum[:I], full[U:], atol=1e-6)
+    assert np.all(item_sum[I:] == 0)
 
 
 def test_lists_to_csr_packing():
