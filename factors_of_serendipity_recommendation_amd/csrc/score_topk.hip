@@ -572,17 +572,18 @@ __global__ __launch_bounds__(256) void score_topk_kernel(ScoreArgs a) {
 // conflict-free ds_read_b128s; the swizzle is applied to the DMA SOURCE address because the LDS
 // destination of an LDS-DMA is lane-linear.  Splits are assigned so that the workgroups one XCD
 // runs concurrently (blockIdx = xcd mod 8) sweep the same catalog slice and share its L2.
-constexpr int kLdsWaves = 8;
-constexpr int kLdsUsers = kLdsWaves * kUsersPerWave;  // 256 users per workgroup
-constexpr int kTileItems = 64;
+// Workgroup shape: WAVES x 32 users, tiles of 32*NACC items.  <8, 2> (one 512-thread workgroup per
+// CU, 64-item tiles) is the one launched; see lds_waves() for the measured alternative.
 
-template <int KSTEPS>
+template <int KSTEPS, int WAVES = 8, int NACC = 2>
 struct LdsGeom {
+    static constexpr int TILE_ITEMS = 32 * NACC;
+    static constexpr int USERS = WAVES * kUsersPerWave;
     static constexpr int RB = KSTEPS * 32;              // bytes per bf16 item row (d = 16*KSTEPS)
     static constexpr int CPR = RB / 16;                 // 16-B chunks per row
-    static constexpr int TILE = kTileItems * RB;        // bytes per tile
+    static constexpr int TILE = TILE_ITEMS * RB;        // bytes per tile
     static constexpr int PIECES = TILE / 1024;          // 1-KiB LDS-DMA wave instructions per tile
-    static constexpr int PPW = (PIECES + kLdsWaves - 1) / kLdsWaves;
+    static constexpr int PPW = (PIECES + WAVES - 1) / WAVES;
     // XOR swizzle inside aligned groups of P chunks, P = the largest power of two (<= 16)
     // dividing CPR, so that chunk ^ (row & SWZ) is a permutation of the row's chunks
     static constexpr int SWZ = ((CPR & -CPR) < 16 ? (CPR & -CPR) : 16) - 1;
@@ -624,9 +625,10 @@ __device__ __forceinline__ uint32_t lds_u32(const void* p) {
 // buffer tile t-1 used (every wave left it at the barrier closing t-1), computes tile t, then
 // waits for its own pieces of tile t+1 (vmcnt leaves the younger tiles' pieces in flight) and
 // joins the barrier that publishes tile t+1 to all waves.
-template <int KSTEPS, bool MINMAX, int ABLATE = 0>
-__global__ __launch_bounds__(512) void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf) {
-    typedef LdsGeom<KSTEPS> G;
+template <int KSTEPS, bool MINMAX, int ABLATE = 0, int WAVES = 8, int NACC = 2>
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf) {
+    typedef LdsGeom<KSTEPS, WAVES, NACC> G;
     typedef Frag<LGX_DTYPE_BF16> F;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* tiles = smem;  // [nbuf][TILE]
@@ -651,7 +653,7 @@ __global__ __launch_bounds__(512) void score_topk_bf16_lds(ScoreArgs a, int xcd_
     }
     if (utile >= n_utiles) return;
 
-    const int64_t b = utile * kLdsUsers + wave * kUsersPerWave + col;
+    const int64_t b = utile * G::USERS + wave * kUsersPerWave + col;
     const bool user_ok = b < a.B;
     const int64_t qrow = user_ok ? (a.user_rows ? a.user_rows[b] : b) : 0;
     typename F::chunk uf[KSTEPS];
@@ -673,7 +675,7 @@ __global__ __launch_bounds__(512) void score_topk_bf16_lds(ScoreArgs a, int xcd_
 
     const int64_t i_begin = (int64_t)split * a.split_items;
     const int64_t i_end = min(a.n_items, i_begin + a.split_items);
-    const int64_t ntiles = i_end > i_begin ? (i_end - i_begin + kTileItems - 1) / kTileItems : 0;
+    const int64_t ntiles = i_end > i_begin ? (i_end - i_begin + G::TILE_ITEMS - 1) / G::TILE_ITEMS : 0;
     // single split: every workgroup sweeps the whole catalog, starting at a rotation shared by the
     // workgroups of its XCD (blockIdx mod 8) so that co-resident workgroups read the same tiles
     const int64_t rot = a.n_splits == 1 ? (bid % 8) * (ntiles / 8) : 0;
@@ -688,11 +690,11 @@ __global__ __launch_bounds__(512) void score_topk_bf16_lds(ScoreArgs a, int xcd_
     auto tile_start = [&](int64_t t) {
         int64_t u = t + rot;
         if (u >= ntiles) u -= ntiles;
-        return i_begin + u * kTileItems;
+        return i_begin + u * G::TILE_ITEMS;
     };
     auto stage = [&](int buf, int64_t t0) {
         const unsigned char* base = items + t0 * G::RB;
-        const bool tail = t0 + kTileItems > i_end;
+        const bool tail = t0 + G::TILE_ITEMS > i_end;
         const int last = (int)(i_end - 1 - t0);  // tail rows re-read the split's last row (masked later)
 #pragma unroll
         for (int p = 0; p < G::PPW; ++p) {
@@ -729,39 +731,37 @@ __global__ __launch_bounds__(512) void score_topk_bf16_lds(ScoreArgs a, int xcd_
         const unsigned char* r1 = T + it1 * G::RB;
         // fragment reads run one k-step ahead of the MFMAs
         uint4 a0 = *reinterpret_cast<const uint4*>(r0 + ((h ^ (it0 & G::SWZ)) * 16));
-        uint4 a1 = *reinterpret_cast<const uint4*>(r1 + ((h ^ (it1 & G::SWZ)) * 16));
+        uint4 a1 = a0;
+        if (NACC == 2) a1 = *reinterpret_cast<const uint4*>(r1 + ((h ^ (it1 & G::SWZ)) * 16));
 #pragma unroll
         for (int c = 0; c < KSTEPS; ++c) {
             uint4 n0 = a0, n1 = a1;
             if (c + 1 < KSTEPS) {
                 const int pch = 2 * (c + 1) + h;
                 n0 = *reinterpret_cast<const uint4*>(r0 + ((pch ^ (it0 & G::SWZ)) * 16));
-                n1 = *reinterpret_cast<const uint4*>(r1 + ((pch ^ (it1 & G::SWZ)) * 16));
+                if (NACC == 2) n1 = *reinterpret_cast<const uint4*>(r1 + ((pch ^ (it1 & G::SWZ)) * 16));
             }
             acc0 = F::mma(a0, uf[c], acc0);
-            acc1 = F::mma(a1, uf[c], acc1);
+            if (NACC == 2) acc1 = F::mma(a1, uf[c], acc1);
             a0 = n0;
             a1 = n1;
         }
-        // keep the reads one k-step ahead: 2 DS reads, then the 2 MFMAs of the previous k-step
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        // keep the reads one k-step ahead: NACC DS reads, then the NACC MFMAs of the previous k-step
+        __builtin_amdgcn_sched_group_barrier(0x100, NACC, 0);
 #pragma unroll
         for (int c = 0; c < KSTEPS; ++c) {
-            if (c + 1 < KSTEPS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            if (c + 1 < KSTEPS) __builtin_amdgcn_sched_group_barrier(0x100, NACC, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, NACC, 0);
         }
-#ifdef LGX_SCORE_STATS
-        const uint64_t stat_t1_ = __builtin_amdgcn_s_memtime();
-#endif
         if (ABLATE == 1) {  // development: MFMA + LDS pipeline only (keeps the accumulators live)
             float z = 0.0f;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) z += acc0[r] + acc1[r];
+            for (int r = 0; r < 16; ++r) z += acc0[r] + (NACC == 2 ? acc1[r] : 0.0f);
             st.mx = fmaxf(st.mx, z);
         } else if (ABLATE == 3) {  // development: filter fast path only
-            st.template block<MINMAX, 2, true>(a, acc0, acc1, t0, i_end);
+            st.template block<MINMAX, NACC, true>(a, acc0, acc1, t0, i_end);
         } else {
-            st.template block<MINMAX, 2>(a, acc0, acc1, t0, i_end);
+            st.template block<MINMAX, NACC>(a, acc0, acc1, t0, i_end);
         }
 #ifdef LGX_SCORE_STATS
         const uint64_t stat_t2_ = __builtin_amdgcn_s_memtime();
@@ -883,7 +883,14 @@ struct SplitPlan {
     bool lds;        // bf16 LDS-DMA kernel
     bool xcd_affine;
     int64_t n_utiles;
+    int waves;       // LDS kernel shape: 4 (two workgroups per CU, 32-item tiles) or 8 (one, 64-item)
 };
+
+// LDS kernel shape.  The two-workgroups-per-CU shape <4, 1> was measured slower (902 vs 1079 TF/s
+// unmasked, 131072 users, d=256): halving the tile doubles the barriers per MFMA, which costs more
+// than the overlap of two independent workgroups recovers.  Only <8, 2> is instantiated.
+inline int lds_waves() { return 8; }
+inline int64_t lds_resident(int waves) { return waves == 4 ? 512 : 256; }  // workgroups at once
 
 // LDS kernel applies to bf16, d a multiple of 32 up to 256 (even k-step counts are instantiated),
 // k <= 32 (LDS budget)
@@ -894,25 +901,28 @@ bool lds_eligible(int dtype, int64_t d, int k) {
 SplitPlan plan_splits(int64_t B, int64_t n_items, int dtype, int64_t d, int k) {
     const int64_t tiles32 = ceil_div(n_items, 32);
     if (lds_eligible(dtype, d, k)) {
-        const int64_t ut = ceil_div(B, kLdsUsers);
-        const int64_t tiles = ceil_div(n_items, kTileItems);
-        if (ut >= 512)  // >= 2 rounds of one workgroup per CU: no catalog split, XCD-rotated sweeps
-            return {1, tiles * kTileItems, true, false, ut};
-        // >= 2 workgroups (512 threads) per CU, >= 4 tiles per split, a multiple of 8 when possible
-        int64_t s = ceil_div(512, ut);
+        const int waves = lds_waves();
+        const int64_t users = waves * kUsersPerWave, tile_items = waves == 4 ? 32 : 64;
+        const int64_t resident = lds_resident(waves);
+        const int64_t ut = ceil_div(B, users);
+        const int64_t tiles = ceil_div(n_items, tile_items);
+        if (ut >= 2 * resident)  // >= 2 full rounds: no catalog split, XCD-rotated sweeps
+            return {1, tiles * tile_items, true, false, ut, waves};
+        // >= 2 rounds of resident workgroups, >= 4 tiles per split, a multiple of 8 when possible
+        int64_t s = ceil_div(2 * resident, ut);
         s = std::min<int64_t>(s, std::max<int64_t>(1, tiles / 4));
         s = std::max<int64_t>(1, std::min<int64_t>(s, 256));
         if (s >= 8) s = s / 8 * 8;
-        const int64_t per = ceil_div(tiles, s) * kTileItems;
+        const int64_t per = ceil_div(tiles, s) * tile_items;
         const int n = (int)ceil_div(n_items, per);
-        return {n, per, true, n % 8 == 0, ut};
+        return {n, per, true, n % 8 == 0, ut, waves};
     }
     const int64_t user_blocks = ceil_div(B, kUsersPerBlock);
     int64_t s = ceil_div(2048, user_blocks);                       // aim for >= ~8 workgroups per CU
     s = std::min<int64_t>(s, std::max<int64_t>(1, tiles32 / 8));  // >= 8 tiles per split
     s = std::max<int64_t>(1, std::min<int64_t>(s, 64));
     const int64_t per = ceil_div(tiles32, s) * 32;
-    return {(int)ceil_div(n_items, per), per, false, false, user_blocks};
+    return {(int)ceil_div(n_items, per), per, false, false, user_blocks, 0};
 }
 
 template <typename KernelT>
@@ -944,49 +954,53 @@ int launch_v1(const ScoreArgs& a, int kch, hipStream_t stream) {
     return LGX_OK;
 }
 
-// tile buffers of the barrier kernel: as many as fit beside the top-k lists, 2..4
+// tile buffers of the LDS kernel: as many as fit beside the top-k lists in the workgroup's share of
+// the CU's LDS, 2..4
 constexpr size_t kLdsBytes = 160 * 1024;
-inline int lds_ring_buffers(size_t tile, size_t lists) {
-    const size_t fit = lists < kLdsBytes ? (kLdsBytes - lists) / tile : 0;
+inline int lds_ring_buffers(size_t tile, size_t lists, int wg_per_cu) {
+    const size_t budget = kLdsBytes / wg_per_cu;
+    const size_t fit = lists < budget ? (budget - lists) / tile : 0;
     return (int)std::max<size_t>(2, std::min<size_t>(4, fit));
+}
+
+template <int KS, bool MM, int ABL, int WAVES, int NACC>
+int launch_lds_shape(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
+    typedef LdsGeom<KS, WAVES, NACC> G;
+    const size_t lists = (size_t)WAVES * list_bytes_per_wave(a.k);
+    const int nbuf = lds_ring_buffers(G::TILE, lists, WAVES == 4 ? 2 : 1);
+    const size_t shmem = (size_t)nbuf * G::TILE + lists;
+    int rc = set_lds_limit(score_topk_bf16_lds<KS, MM, ABL, WAVES, NACC>, shmem);
+    if (rc) return rc;
+    const unsigned grid = (unsigned)(p.n_utiles * p.n_splits);
+    score_topk_bf16_lds<KS, MM, ABL, WAVES, NACC><<<grid, WAVES * 64, shmem, stream>>>(
+        a, p.xcd_affine ? 1 : 0, p.n_utiles, nbuf);
+    LGX_LAUNCH_CHECK();
+    return LGX_OK;
 }
 
 template <bool MM, int ABL = 0>
 int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     const int ksteps = (int)(a.d / 16);
-    const unsigned grid = (unsigned)(p.n_utiles * p.n_splits);
-#define LGX_SL(KS)                                                                                          \
-    do {                                                                                                    \
-        const size_t lists = (size_t)kLdsWaves * list_bytes_per_wave(a.k);                                   \
-        const int nbuf = lds_ring_buffers(LdsGeom<KS>::TILE, lists);                                         \
-        const size_t shmem = (size_t)nbuf * LdsGeom<KS>::TILE + lists;                                       \
-        int rc_ = set_lds_limit(score_topk_bf16_lds<KS, MM, ABL>, shmem);                                 \
-        if (rc_) return rc_;                                                                                \
-        score_topk_bf16_lds<KS, MM, ABL><<<grid, 512, shmem, stream>>>(a, p.xcd_affine ? 1 : 0, p.n_utiles, \
-                                                                       nbuf);                               \
-    } while (0)
+#define LGX_SL(KS) return launch_lds_shape<KS, MM, ABL, 8, 2>(a, p, stream)
     switch (ksteps) {
-        case 2: LGX_SL(2); break;
-        case 4: LGX_SL(4); break;
-        case 6: LGX_SL(6); break;
-        case 8: LGX_SL(8); break;
-        case 10: LGX_SL(10); break;
-        case 12: LGX_SL(12); break;
-        case 14: LGX_SL(14); break;
-        case 16: LGX_SL(16); break;
+        case 2: LGX_SL(2);
+        case 4: LGX_SL(4);
+        case 6: LGX_SL(6);
+        case 8: LGX_SL(8);
+        case 10: LGX_SL(10);
+        case 12: LGX_SL(12);
+        case 14: LGX_SL(14);
+        case 16: LGX_SL(16);
         default:
             set_error("lgx_score_topk: no LDS kernel for d=%lld", (long long)a.d);
             return LGX_ERR_UNSUPPORTED;
     }
 #undef LGX_SL
-    LGX_LAUNCH_CHECK();
-    return LGX_OK;
 }
 
-// A batch runs as up to two launches over user ranges.  The LDS kernel's full-sweep mode runs
-// one workgroup per CU per round; when the last round would leave most CUs idle, the users of that
-// partial round become a second launch whose catalog splits fill the chip.
-constexpr int64_t kRoundTiles = 256;  // workgroups resident at once (one per CU)
+// A batch runs as up to two launches over user ranges.  In the LDS kernel's full-sweep mode every
+// round runs the resident workgroups; when the last round would leave most of them idle, the users
+// of that partial round become a second launch whose catalog splits fill the chip.
 struct UserRange {
     int64_t u0, u1;
     SplitPlan p;
@@ -997,9 +1011,10 @@ int plan_ranges(int64_t B, int64_t n_items, int dtype, int64_t d, int k, UserRan
     const SplitPlan p = plan_splits(B, n_items, dtype, d, k);
     int n = 0;
     int64_t full = B;
-    if (p.lds && p.n_splits == 1 && p.n_utiles >= 2 * kRoundTiles) {  // full-sweep mode
-        const int64_t rem_tiles = p.n_utiles % kRoundTiles;
-        if (rem_tiles != 0 && rem_tiles < kRoundTiles * 3 / 4) full = (p.n_utiles - rem_tiles) * kLdsUsers;
+    const int64_t resident = lds_resident(p.waves);
+    if (p.lds && p.n_splits == 1 && p.n_utiles >= 2 * resident) {  // full-sweep mode
+        const int64_t rem_tiles = p.n_utiles % resident;
+        if (rem_tiles != 0 && rem_tiles < resident * 3 / 4) full = (p.n_utiles - rem_tiles) * p.waves * kUsersPerWave;
     }
     size_t off = 0;
     r[n++] = {0, full, plan_splits(full, n_items, dtype, d, k), 0};
