@@ -21,6 +21,7 @@ LGX_OK = 0
 LGX_DTYPE_F32 = 0
 LGX_DTYPE_BF16 = 1
 LGX_LAYER_PLAIN, LGX_LAYER_FIRST, LGX_LAYER_MID, LGX_LAYER_LAST, LGX_LAYER_ONLY, LGX_LAYER_PARTIAL = range(6)
+LGX_REDUCE_MAX, LGX_REDUCE_SUM = 0, 1
 
 _c_i64 = ctypes.c_int64
 _c_int = ctypes.c_int
@@ -53,6 +54,7 @@ SIGNATURES = {
     "lgx_propagate_layer": (_c_int, [ctypes.POINTER(LgxCSR), _vp, _vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int,
                                      ctypes.c_float, _vp]),
     "lgx_spmm_csr": (_c_int, [ctypes.POINTER(LgxCSR), _vp, _vp, _c_i64, _c_int, _vp]),
+    "lgx_list_dot_reduce": (_c_int, [_vp, _c_i64, _c_int, _c_i64, _vp, _vp, _vp, _vp, _c_int, _vp, _vp]),
     "lgx_layer_epilogue": (_c_int, [_vp, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_float, _vp]),
     "lgx_propagate_workspace": (_c_int, [_c_i64, _c_i64, _c_int, _sz_p]),
     "lgx_propagate": (_c_int, [ctypes.POINTER(LgxCSR), _vp, _vp, _c_i64, _c_int, _c_int, _vp, ctypes.c_size_t, _vp]),

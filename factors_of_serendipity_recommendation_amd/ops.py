@@ -128,6 +128,26 @@ def lists_to_device_csr(lists: Sequence[Sequence[int]], device, sort: bool = Tru
     return torch.from_numpy(indptr).to(device), torch.from_numpy(flat).to(device)
 
 
+def list_dot_reduce(table: torch.Tensor, a_csr: Tuple[torch.Tensor, torch.Tensor],
+                    b_csr: Tuple[torch.Tensor, torch.Tensor], reduce: str = "max") -> torch.Tensor:
+    """``lgx_list_dot_reduce``: per user u, for each a in A(u) the max (or sum) over b in B(u) of
+    <table[a], table[b]>.  a_csr / b_csr = (indptr int64 [U+1], items int32) on the device (same U).
+    Returns f32 [nnz(A)] in A's order (-inf / 0 for an empty B(u))."""
+    require_gpu(table)
+    (ap, ai), (bp, bi) = a_csr, b_csr
+    if ap.shape != bp.shape:
+        raise ValueError("A and B must list the same users")
+    table = table.contiguous()
+    n_users = ap.shape[0] - 1
+    n = int(ap[-1].item()) if n_users > 0 else 0
+    out = torch.empty(max(n, 1), dtype=torch.float32, device=table.device)
+    red = _lib.LGX_REDUCE_MAX if reduce == "max" else _lib.LGX_REDUCE_SUM
+    _lib.check(_lib.lib().lgx_list_dot_reduce(table.data_ptr(), table.shape[1], _dtype_code(table), n_users,
+                                              ap.data_ptr(), ai.data_ptr(), bp.data_ptr(), bi.data_ptr(), red,
+                                              out.data_ptr(), _stream_ptr(table.device)), "lgx_list_dot_reduce")
+    return out[:n]
+
+
 def score_topk(Q: torch.Tensor, items: torch.Tensor, k: int, user_rows: Optional[torch.Tensor] = None,
                mask: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, mask_value: float = float("-inf"),
                apply_sigmoid: bool = False, want_minmax: bool = False):

@@ -1,10 +1,14 @@
-"""recommend.py similarity drop-ins on the GPU (rows a11 / a12 of SURVEY.md section 8).
+"""recommend.py similarity drop-ins on the GPU (rows a11 / a12 and 8(f) rank 1 of SURVEY.md).
 
   accuracy_cf          recommend.py:208-223 (+ sub_argpartition :53-56): per user, dot products of
                        E_u with the user's ~1000 candidate items, top-K -> data/<ds>/rec/<seed>/rec_acc.npy
   similarity_minmax    recommend.py:163-164 (elasticity_item) and :375-377 (stratification):
                        global min / max of E_user . E_item^T, computed inside the fused scoring
                        kernel without materialising the [U, I] matrix
+  difference           recommend.py:287-312: per candidate, max dot with the user's train items
+                       (lgx_list_dot_reduce), scaled by the item . item^T min / max -> rec_dif.npy
+  elasticity_item      recommend.py:149-205 (+ :144-145): scaled user-candidate dot plus the user's
+                       elasticity; the K candidates closest to alpha * mean -> rec_ela.npy
 
 Same signatures and side effects as the reference.  The per-user work runs in lgx_gather_scores +
 lgx_topk_rows instead of a Python loop feeding a multiprocessing.Pool.  The reference's
@@ -32,16 +36,14 @@ def candidate_scores(emb_user: torch.Tensor, emb_item: torch.Tensor,
     return ops.gather_scores(emb_user, emb_item, (indptr, items), n_pairs), indptr, items
 
 
-def topk_candidates(emb_user: torch.Tensor, emb_item: torch.Tensor, candidates: Sequence[Sequence[int]],
-                    K: int = 20) -> np.ndarray:
-    """For each user the K candidate items with the largest <E_u, E_i> -> int64 [U, K]."""
-    scores, indptr, items = candidate_scores(emb_user, emb_item, candidates)
-    U = len(candidates)
+def ragged_topk(scores: torch.Tensor, indptr: torch.Tensor, items: torch.Tensor, K: int) -> np.ndarray:
+    """Per user, the K list entries with the largest f32 score (descending, ties -> earlier position):
+    the ragged scores are packed into a -inf padded [U, width] matrix for lgx_topk_rows."""
+    U = indptr.shape[0] - 1
     lens = torch.diff(indptr)
     width = int(lens.max().item()) if U else 0
     if width < K:
         raise ValueError(f"every user needs at least K={K} candidates")
-    # pack the ragged scores into a padded [U, width] matrix (-inf padding never wins)
     dense = torch.full((U, width), float("-inf"), dtype=torch.float32, device=scores.device)
     rows = torch.repeat_interleave(torch.arange(U, device=scores.device), lens)
     cols = torch.arange(scores.numel(), device=scores.device) - indptr[:-1][rows]
@@ -49,6 +51,13 @@ def topk_candidates(emb_user: torch.Tensor, emb_item: torch.Tensor, candidates: 
     pos, _ = ops.topk_rows(dense, K)
     picked = items.long()[indptr[:-1, None] + pos.long()]
     return picked.cpu().numpy().astype(np.int64)
+
+
+def topk_candidates(emb_user: torch.Tensor, emb_item: torch.Tensor, candidates: Sequence[Sequence[int]],
+                    K: int = 20) -> np.ndarray:
+    """For each user the K candidate items with the largest <E_u, E_i> -> int64 [U, K]."""
+    scores, indptr, items = candidate_scores(emb_user, emb_item, candidates)
+    return ragged_topk(scores, indptr, items, K)
 
 
 def accuracy_cf(mat_candidate: Dict[int, List[int]], dataset_name: str, seed: int, K: int = 20,
@@ -71,3 +80,75 @@ def similarity_minmax(emb_user: torch.Tensor, emb_item: torch.Tensor) -> Tuple[f
     _, _, mm = ops.score_topk(emb_user.contiguous(), emb_item.contiguous(), 1, want_minmax=True)
     mm = mm.cpu().numpy()
     return float(mm[0]), float(mm[1])
+
+
+def item_dot_minmax(emb_item: torch.Tensor) -> Tuple[float, float]:
+    """(min, max) of emb_item . emb_item^T (recommend.py:291-292; utils.py:500-529's blocked loop)."""
+    return similarity_minmax(emb_item, emb_item)
+
+
+def train_lists(dataset_name: str, n_users: int, data_root: str = "data") -> List[List[int]]:
+    """rating_train.csv grouped by userInd, the i-th group for user i (the reference zips the groups
+    with range(len(mat_candidate)), recommend.py:297-298)."""
+    import pandas as pd
+    df = pd.read_csv(os.path.join(data_root, dataset_name, "rating_train.csv"), usecols=["userInd", "itemInd"])
+    groups = [g["itemInd"].values.tolist() for _, g in df.groupby("userInd")]
+    return groups[:n_users]
+
+
+def difference_scores(emb_item: torch.Tensor, candidates: Sequence[Sequence[int]],
+                      history: Sequence[Sequence[int]]) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """diffscore = 1 - (max_t <E_c, E_t> - min_dis) / (max_dis - min_dis) per candidate c of each user,
+    max over the user's history t (recommend.py:305-307)."""
+    dev = emb_item.device
+    a = ops.lists_to_device_csr(candidates, dev, sort=False)
+    b = ops.lists_to_device_csr(history, dev, sort=False)
+    m = ops.list_dot_reduce(emb_item, a, b, "max")
+    mn, mx = item_dot_minmax(emb_item)
+    return 1.0 - (m - mn) / (mx - mn), a[0], a[1]
+
+
+def difference(mat_candidate: Dict[int, List[int]], dataset_name: str, seed: int, K: int = 20,
+               data_root: str = "data", device="cuda") -> None:
+    """recommend.difference: same inputs (emb_item.npy, rating_train.csv, candidates), same output
+    data/<ds>/rec/<seed>/rec_dif.npy [U, K] (the top-K set by diffscore, here ordered)."""
+    emb_item = np.load(os.path.join(data_root, dataset_name, "emb_item.npy"), allow_pickle=False)
+    ei = torch.from_numpy(np.ascontiguousarray(emb_item, dtype=np.float32)).to(device)
+    cands = [mat_candidate[u] for u in range(len(mat_candidate))]
+    scores, indptr, items = difference_scores(ei, cands, train_lists(dataset_name, len(cands), data_root))
+    out_dir = os.path.join(data_root, dataset_name, "rec", str(seed))
+    os.makedirs(out_dir, exist_ok=True)
+    np.save(os.path.join(out_dir, "rec_dif.npy"), ragged_topk(scores, indptr, items, K))
+
+
+def elasticity_keys(emb_user: torch.Tensor, emb_item: torch.Tensor, candidates: Sequence[Sequence[int]],
+                    num_item: np.ndarray, alpha: float = 1.0) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """-|factor - alpha * mean(factor)| per candidate (larger = closer), factor = scaled user-candidate
+    dot + the user's min-max scaled item count (recommend.py:162-185); float64 as in the reference."""
+    scores, indptr, items = candidate_scores(emb_user, emb_item, candidates)
+    mn, mx = similarity_minmax(emb_user, emb_item)
+    cnt = torch.as_tensor(np.asarray(num_item, dtype=np.float64), device=scores.device)
+    ela = (cnt - cnt.min()) / (cnt.max() - cnt.min())
+    lens = torch.diff(indptr)
+    rows = torch.repeat_interleave(torch.arange(len(candidates), device=scores.device), lens)
+    factor = (scores.double() - mn) / (mx - mn) + ela[rows]
+    key = -(factor - alpha * factor.mean()).abs()
+    return key.float(), indptr, items
+
+
+def elasticity_item(mat_candidate: Dict[int, List[int]], dataset_name: str, seed: int, K: int = 20,
+                    alpha: float = 1.0, data_root: str = "data", device="cuda", **kwargs) -> None:
+    """recommend.elasticity_item: same inputs (user.csv num_item, emb_{user,item}.npy, candidates),
+    same output data/<ds>/rec/<seed>/rec_ela.npy [U, K] (the K candidates with the smallest
+    |factor - alpha * mean|, here ordered by that distance)."""
+    import pandas as pd
+    df_user = pd.read_csv(os.path.join(data_root, dataset_name, "user.csv"))
+    emb_item = np.load(os.path.join(data_root, dataset_name, "emb_item.npy"), allow_pickle=False)
+    emb_user = np.load(os.path.join(data_root, dataset_name, "emb_user.npy"), allow_pickle=False)
+    eu = torch.from_numpy(np.ascontiguousarray(emb_user, dtype=np.float32)).to(device)
+    ei = torch.from_numpy(np.ascontiguousarray(emb_item, dtype=np.float32)).to(device)
+    cands = [mat_candidate[u] for u in range(len(mat_candidate))]
+    key, indptr, items = elasticity_keys(eu, ei, cands, df_user["num_item"].values, alpha)
+    out_dir = os.path.join(data_root, dataset_name, "rec", str(seed))
+    os.makedirs(out_dir, exist_ok=True)
+    np.save(os.path.join(out_dir, "rec_ela.npy"), ragged_topk(key, indptr, items, K))

@@ -25,6 +25,8 @@
  *   lgx_topk_rows          c_top_k_array_index                  LightGCN-tf/evaluator/cpp/include/tools.h:13-33
  *   lgx_foldout_metrics    evaluate_foldout                     LightGCN-tf/evaluator/cpp/include/evaluate_foldout.h:115-195
  *   lgx_gather_scores      accuracy_cf / elasticity_item per-user candidate dot  recommend.py:167-171, 214-217
+ *   lgx_list_dot_reduce    difference / ser1 / ser2 / diversity per-user list products
+ *                          recommend.py:305-307; utils.py:34-35, 117-121, 265-267
  */
 #ifndef LGX_H
 #define LGX_H
@@ -185,6 +187,21 @@ int lgx_foldout_metrics(const int32_t* rankings, int64_t users, int k, const int
 int lgx_gather_scores(const float* emb_user, const float* emb_item, int64_t n_users, int64_t d,
                       const int64_t* cand_indptr, const int32_t* cand_items, int64_t n_pairs,
                       float* scores, lgx_stream_t stream);
+
+/* ---------------------------------------------------------------- 8(f) rank 1: list x list similarity */
+#define LGX_REDUCE_MAX 0
+#define LGX_REDUCE_SUM 1
+/*
+ * For every user u (ragged lists A and B as CSR: indptr [U+1] int64, items int32 rows of `table`):
+ *   out[p] = max (or sum) over b in B(u) of <table[a_items[p]], table[b]>,  p in [a_indptr[u], a_indptr[u+1]).
+ * An empty B(u) gives -inf (max) / 0 (sum).  table [rows, d] f32 or bf16 (fp32 accumulation).
+ * Replaces the per-user numpy products of recommend.difference (recommend.py:305-307),
+ * utils.ser1_sub (utils.py:34-35), utils.ser2_sub (utils.py:117-121), utils.diversity_sub
+ * (utils.py:265-267).
+ */
+int lgx_list_dot_reduce(const void* table, int64_t d, int dtype, int64_t n_users, const int64_t* a_indptr,
+                        const int32_t* a_items, const int64_t* b_indptr, const int32_t* b_items, int reduce,
+                        float* out, lgx_stream_t stream);
 
 /* ---------------------------------------------------------------- synthetic graphs (bench) */
 /*

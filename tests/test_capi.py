@@ -18,7 +18,8 @@ def declared_functions():
 def test_header_declares_expected_entry_points():
     names = declared_functions()
     for n in ["lgx_build_norm_adj", "lgx_propagate", "lgx_propagate_layer", "lgx_spmm_csr", "lgx_score_topk",
-              "lgx_score_dense", "lgx_topk_rows", "lgx_foldout_metrics", "lgx_gather_scores", "lgx_version"]:
+              "lgx_score_dense", "lgx_topk_rows", "lgx_foldout_metrics", "lgx_gather_scores", "lgx_version",
+              "lgx_list_dot_reduce", "lgx_layer_epilogue"]:
         assert n in names
 
 
@@ -56,3 +57,17 @@ def test_ops_refuse_cpu_tensors():
         lgx.topk_rows(torch.zeros(2, 4), 1)
     with pytest.raises(RuntimeError, match="GPU only"):
         lgx.score_topk(torch.zeros(2, 8), torch.zeros(3, 8), 1)
+
+
+def test_new_entry_points_reject_bad_arguments_before_device_work():
+    from factors_of_serendipity_recommendation_amd import _lib
+    L = _lib.lib()
+    p = ctypes.c_void_p(16)
+    # unknown reduction
+    assert L.lgx_list_dot_reduce(p, 64, 0, 1, p, p, p, p, 7, p, None) == 1
+    # d beyond the kernel's register budget
+    assert L.lgx_list_dot_reduce(p, 300, 0, 1, p, p, p, p, 0, p, None) == 3
+    assert b"d=300" in L.lgx_last_error()
+    # the epilogue has no PARTIAL mode, and needs its buffers
+    assert L.lgx_layer_epilogue(p, 4, p, p, p, p, 64, 0, _lib.LGX_LAYER_PARTIAL, 1.0, None) == 1
+    assert L.lgx_layer_epilogue(p, 4, None, p, p, p, 64, 0, _lib.LGX_LAYER_FIRST, 1.0, None) == 1
