@@ -1,0 +1,63 @@
+"""BPR training drop-ins: utils.BPRLoss (code/utils.py:34-53) and
+Procedure.BPR_train_original (code/Procedure.py:26-57).
+
+Same semantics, with the epoch's samples drawn on the GPU (``sampling.sample_device``) and shuffled
+and batched on the device -- nothing goes through the host.  Every minibatch runs the model's
+``bpr_loss``: for the LightGCN module of this package that is the HIP propagation forward and, in
+backward, the same K-layer propagation of the gradient (A^ is symmetric), then torch's Adam.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+from torch import optim
+
+from . import sampling
+
+
+class BPRLoss:
+    """utils.BPRLoss: Adam on the model's parameters, loss = bpr + decay * reg."""
+
+    def __init__(self, recmodel, config: dict):
+        self.model = recmodel
+        self.weight_decay = config["decay"]
+        self.lr = config["lr"]
+        self.opt = optim.Adam(recmodel.parameters(), lr=self.lr)
+
+    def stageOne(self, users, pos, neg) -> float:
+        loss, reg_loss = self.model.bpr_loss(users, pos, neg)
+        loss = loss + reg_loss * self.weight_decay
+        self.opt.zero_grad()
+        loss.backward()
+        self.opt.step()
+        return loss.detach()
+
+
+def _positives(dataset, device):
+    if not hasattr(dataset, "_lgx_pos_csr"):
+        dataset._lgx_pos_csr = sampling._positives(dataset.allPos, device)
+    return dataset._lgx_pos_csr
+
+
+def BPR_train_original(dataset, recommend_model, loss_class: BPRLoss, epoch: int, neg_k: int = 1, w=None,
+                       batch_size: int = 2048, device="cuda") -> str:
+    """Procedure.BPR_train_original: one epoch of BPR minibatches; returns the same summary string."""
+    Recmodel = recommend_model
+    Recmodel.train()
+    t0 = time.perf_counter()
+    pos = _positives(dataset, device)
+    per = max(1, dataset.trainDataSize // max(1, dataset.n_users))
+    S = sampling.sample_device(pos, dataset.m_items, per_user=per, neg_num=neg_k).long()
+    t_sample = time.perf_counter() - t0
+    perm = torch.randperm(S.shape[0], device=S.device)  # utils.shuffle
+    users, posItems, negItems = S[perm, 0], S[perm, 1], S[perm, 2]
+    total_batch = len(users) // batch_size + 1
+    aver_loss = torch.zeros((), device=S.device)
+    for batch_i, i in enumerate(range(0, len(users), batch_size)):  # utils.minibatch
+        cri = loss_class.stageOne(users[i:i + batch_size], posItems[i:i + batch_size], negItems[i:i + batch_size])
+        aver_loss += cri
+        if w is not None:
+            w.add_scalar("BPRLoss/BPR", float(cri), epoch * int(len(users) / batch_size) + batch_i)
+    aver_loss = float(aver_loss) / total_batch
+    return f"loss{aver_loss:.3f}-|Sample:{t_sample:.2f}|"

@@ -25,6 +25,7 @@
  *   lgx_topk_rows          c_top_k_array_index                  LightGCN-tf/evaluator/cpp/include/tools.h:13-33
  *   lgx_foldout_metrics    evaluate_foldout                     LightGCN-tf/evaluator/cpp/include/evaluate_foldout.h:115-195
  *   lgx_gather_scores      accuracy_cf / elasticity_item per-user candidate dot  recommend.py:167-171, 214-217
+ *   lgx_sample_bpr         sample_negative / sample_negative_ByUser   sources/sampling.cpp:27-86
  *   lgx_list_dot_reduce    difference / ser1 / ser2 / diversity per-user list products
  *                          recommend.py:305-307; utils.py:34-35, 117-121, 265-267
  */
@@ -187,6 +188,20 @@ int lgx_foldout_metrics(const int32_t* rankings, int64_t users, int k, const int
 int lgx_gather_scores(const float* emb_user, const float* emb_item, int64_t n_users, int64_t d,
                       const int64_t* cand_indptr, const int32_t* cand_items, int64_t n_pairs,
                       float* scores, lgx_stream_t stream);
+
+/* ---------------------------------------------------------------- 8(f) rank 2: BPR sampling */
+/*
+ * BPR rows out [n_rows, 2 + neg_num] int32 = [user, a positive, neg_num non-positive items]
+ * (sources/sampling.cpp:27-86).  Positives: CSR pos_indptr [n_users+1] int64 / pos_items int32,
+ * each user's list SORTED ascending.  users == NULL: row r belongs to user r / per_user
+ * (sample_negative, per_user = train_num / user_num); else to users[r] (sample_negative_ByUser).
+ * Counter-based draws from `seed` (deterministic per seed; the reference's libc rand() stream is
+ * not reproduced).  A user without positives, or an out-of-range user id, gives -1 in its columns
+ * 1..; a negative that 4096 draws could not find is -1.
+ */
+int lgx_sample_bpr(const int64_t* pos_indptr, const int32_t* pos_items, int64_t n_users, int64_t n_items,
+                   const int32_t* users, int64_t n_rows, int64_t per_user, int neg_num, uint64_t seed,
+                   int32_t* out, lgx_stream_t stream);
 
 /* ---------------------------------------------------------------- 8(f) rank 1: list x list similarity */
 #define LGX_REDUCE_MAX 0

@@ -71,3 +71,15 @@ def test_new_entry_points_reject_bad_arguments_before_device_work():
     # the epilogue has no PARTIAL mode, and needs its buffers
     assert L.lgx_layer_epilogue(p, 4, p, p, p, p, 64, 0, _lib.LGX_LAYER_PARTIAL, 1.0, None) == 1
     assert L.lgx_layer_epilogue(p, 4, None, p, p, p, 64, 0, _lib.LGX_LAYER_FIRST, 1.0, None) == 1
+
+
+def test_sampler_rejects_bad_arguments_before_device_work():
+    from factors_of_serendipity_recommendation_amd import _lib
+    L = _lib.lib()
+    p = ctypes.c_void_p(16)
+    # no user list and no rows per user
+    assert L.lgx_sample_bpr(p, p, 10, 100, None, 10, 0, 1, 1, p, None) == 1
+    # more rows than users * per_user
+    assert L.lgx_sample_bpr(p, p, 10, 100, None, 101, 10, 1, 1, p, None) == 1
+    # empty catalog
+    assert L.lgx_sample_bpr(p, p, 10, 0, None, 10, 1, 1, 1, p, None) == 1
