@@ -54,6 +54,9 @@ SIGNATURES = {
     "lgx_propagate_layer": (_c_int, [ctypes.POINTER(LgxCSR), _vp, _vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int,
                                      ctypes.c_float, _vp]),
     "lgx_spmm_csr": (_c_int, [ctypes.POINTER(LgxCSR), _vp, _vp, _c_i64, _c_int, _vp]),
+    "lgx_parse_lines_workspace": (_c_int, [_c_i64, _sz_p]),
+    "lgx_parse_lines_count": (_c_int, [_vp, _c_i64, _vp, ctypes.c_size_t, _vp, _vp]),
+    "lgx_parse_lines_fill": (_c_int, [_vp, _c_i64, _vp, ctypes.c_size_t, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp]),
     "lgx_sample_bpr": (_c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, _c_int, ctypes.c_uint64, _vp, _vp]),
     "lgx_list_dot_reduce": (_c_int, [_vp, _c_i64, _c_int, _c_i64, _vp, _vp, _vp, _vp, _c_int, _vp, _vp]),
     "lgx_layer_epilogue": (_c_int, [_vp, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_float, _vp]),

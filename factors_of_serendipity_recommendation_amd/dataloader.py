@@ -22,8 +22,14 @@ from .graph import CSRGraph, build_norm_adj, from_csr_arrays
 DEFAULT_CONFIG = {"A_split": False, "A_n_fold": 100}
 
 
-def read_interactions(path: str):
-    """Parse one LightGCN txt file -> (uids, items-per-line lists) (dataloader.py:247-260)."""
+def read_interactions(path: str, device=None):
+    """Parse one LightGCN txt file -> (uids, items-per-line lists) (dataloader.py:247-260).
+    On a CUDA device the bytes are parsed by the GPU (``ops.read_interactions_device``)."""
+    if device is not None and torch.device(device).type == "cuda":
+        from .ops import read_interactions_device
+        lu, lp, it, _ = read_interactions_device(path, device)
+        lu, lp, it = lu.cpu().numpy(), lp.cpu().numpy(), it.cpu().numpy().astype(np.int64)
+        return lu.tolist(), [it[lp[j]:lp[j + 1]] for j in range(len(lu))]
     uids: List[int] = []
     rows: List[np.ndarray] = []
     with open(path) as f:
@@ -46,8 +52,8 @@ class Loader:
         self.path = path
         self.device = torch.device(device)
         self.cache_adj = cache_adj
-        tr_uids, tr_rows = read_interactions(os.path.join(path, "train.txt"))
-        te_uids, te_rows = read_interactions(os.path.join(path, "test.txt"))
+        tr_uids, tr_rows = read_interactions(os.path.join(path, "train.txt"), self.device)
+        te_uids, te_rows = read_interactions(os.path.join(path, "test.txt"), self.device)
         self.trainUniqueUsers = np.asarray(tr_uids)
         self.trainUser = np.concatenate([np.full(len(r), u) for u, r in zip(tr_uids, tr_rows)]) if tr_rows else np.zeros(0, np.int64)
         self.trainItem = np.concatenate(tr_rows) if tr_rows else np.zeros(0, np.int64)

@@ -128,6 +128,39 @@ def lists_to_device_csr(lists: Sequence[Sequence[int]], device, sort: bool = Tru
     return torch.from_numpy(indptr).to(device), torch.from_numpy(flat).to(device)
 
 
+def parse_lines(text: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+    """``lgx_parse_lines_*`` on a device uint8 tensor of "uid item item ..." text ->
+    (line_user int32 [L], line_ptr int64 [L+1], items int32 [P], pair_user int32 [P])."""
+    require_gpu(text)
+    if text.dtype != torch.uint8 or not text.is_contiguous():
+        raise ValueError("text must be a contiguous uint8 tensor")
+    L = _lib.lib()
+    n, dev, st = text.numel(), text.device, _stream_ptr(text.device)
+    wsb = ctypes.c_size_t()
+    _lib.check(L.lgx_parse_lines_workspace(n, ctypes.byref(wsb)), "lgx_parse_lines_workspace")
+    ws = torch.empty(max(wsb.value, 1), dtype=torch.uint8, device=dev)
+    counts = torch.zeros(2, dtype=torch.int64, device=dev)
+    _lib.check(L.lgx_parse_lines_count(text.data_ptr(), n, ws.data_ptr(), wsb.value, counts.data_ptr(), st),
+               "lgx_parse_lines_count")
+    n_numbers, n_lines = (int(x) for x in counts.tolist())
+    n_pairs = n_numbers - n_lines
+    line_user = torch.empty(max(n_lines, 1), dtype=torch.int32, device=dev)
+    line_ptr = torch.empty(n_lines + 1, dtype=torch.int64, device=dev)
+    items = torch.empty(max(n_pairs, 1), dtype=torch.int32, device=dev)
+    pair_user = torch.empty(max(n_pairs, 1), dtype=torch.int32, device=dev)
+    _lib.check(L.lgx_parse_lines_fill(text.data_ptr(), n, ws.data_ptr(), wsb.value, n_numbers, n_lines,
+                                      line_user.data_ptr(), line_ptr.data_ptr(), items.data_ptr(),
+                                      pair_user.data_ptr(), st), "lgx_parse_lines_fill")
+    return line_user[:n_lines], line_ptr, items[:n_pairs], pair_user[:n_pairs]
+
+
+def read_interactions_device(path: str, device="cuda"):
+    """A LightGCN txt file parsed on the device (one host->device copy of its bytes)."""
+    import numpy as np
+    data = np.fromfile(path, dtype=np.uint8)
+    return parse_lines(torch.from_numpy(data).to(device))
+
+
 def list_dot_reduce(table: torch.Tensor, a_csr: Tuple[torch.Tensor, torch.Tensor],
                     b_csr: Tuple[torch.Tensor, torch.Tensor], reduce: str = "max") -> torch.Tensor:
     """``lgx_list_dot_reduce``: per user u, for each a in A(u) the max (or sum) over b in B(u) of

@@ -25,6 +25,7 @@
  *   lgx_topk_rows          c_top_k_array_index                  LightGCN-tf/evaluator/cpp/include/tools.h:13-33
  *   lgx_foldout_metrics    evaluate_foldout                     LightGCN-tf/evaluator/cpp/include/evaluate_foldout.h:115-195
  *   lgx_gather_scores      accuracy_cf / elasticity_item per-user candidate dot  recommend.py:167-171, 214-217
+ *   lgx_parse_lines_*      Loader / Data file parsing            code/dataloader.py:247-277; load_data.py:27-48
  *   lgx_sample_bpr         sample_negative / sample_negative_ByUser   sources/sampling.cpp:27-86
  *   lgx_list_dot_reduce    difference / ser1 / ser2 / diversity per-user list products
  *                          recommend.py:305-307; utils.py:34-35, 117-121, 265-267
@@ -188,6 +189,23 @@ int lgx_foldout_metrics(const int32_t* rankings, int64_t users, int k, const int
 int lgx_gather_scores(const float* emb_user, const float* emb_item, int64_t n_users, int64_t d,
                       const int64_t* cand_indptr, const int32_t* cand_items, int64_t n_pairs,
                       float* scores, lgx_stream_t stream);
+
+/* ---------------------------------------------------------------- 8(f) rank 3: interaction files */
+/*
+ * "uid item item ..." text (dataloader.py:247-277, load_data.py:27-48) parsed on the device in two
+ * passes over the same workspace (lgx_parse_lines_workspace):
+ *   count: counts_out[0] = numbers in the text, counts_out[1] = lines holding a number (device int64[2])
+ *   fill:  line_user [n_lines], line_ptr [n_lines+1] (CSR of each line's items), items [n_numbers - n_lines],
+ *          pair_user [n_numbers - n_lines] (optional: the user of every item, file order).
+ * A number is a run of decimal digits (int32, saturating); any other byte separates; '
+' ends a line.
+ */
+int lgx_parse_lines_workspace(int64_t n_bytes, size_t* ws_bytes);
+int lgx_parse_lines_count(const uint8_t* text, int64_t n_bytes, void* ws, size_t ws_bytes, int64_t* counts_out,
+                          lgx_stream_t stream);
+int lgx_parse_lines_fill(const uint8_t* text, int64_t n_bytes, const void* ws, size_t ws_bytes, int64_t n_numbers,
+                         int64_t n_lines, int32_t* line_user, int64_t* line_ptr, int32_t* items, int32_t* pair_user,
+                         lgx_stream_t stream);
 
 /* ---------------------------------------------------------------- 8(f) rank 2: BPR sampling */
 /*
