@@ -1,0 +1,210 @@
+// stratified candidate sets on the GPU.
+//
+// Reference: recommend.create_candidates_stratification (recommend.py:359-452) with
+// create_candidates_stratification_sub / sample_list (:314-356):
+//   mat_dis   = (E_user . E_item^T).astype(float16)                                   (:375)
+//   label     = floor((mat_dis - min_dis) / inter).astype(int8),
+//               inter = (max(mat_dis) + epsilon - min(mat_dis)) / num_fold           (:377-381)
+//   per user: the items outside its train set, grouped by label; from every group
+//             rint(K * |group| / |items|) items at random, shuffled; then sample_list pads (by
+//             re-drawing from the list) or trims the list to K                         (:327-356)
+//
+// lgx_strat_labels   one workgroup per user row of precomputed fp32 scores: the float16 arithmetic
+//                    of numpy (each operation in float, rounded to half), the train mask (label -1)
+//                    and the per-user label histogram (LDS atomics, one global add per bin).
+// lgx_strat_select   one workgroup per user: every eligible item gets a 64-bit counter-hash key, and
+//                    a radix select over 8 x 8-bit digits -- all labels at once, histograms in LDS --
+//                    finds each label's threshold so that exactly its n smallest keys are taken: a
+//                    uniform random subset.  The picks are ordered by key (a random order, fixed by the
+//                    seed) and padded / trimmed to K as sample_list does.  The reference draws with
+//                    pandas' global numpy generator, so the sets match in distribution, not in bits.
+#include "lgx_common.h"
+
+#include <hip/hip_fp16.h>
+
+namespace lgx {
+namespace {
+
+constexpr int kStratThreads = 256;
+constexpr int kMaxFolds = 32;
+constexpr int kMaxStratK = 1024;  // candidates per user that the selection kernel keeps in LDS
+
+__device__ __forceinline__ float half_round(float x) { return __half2float(__float2half_rn(x)); }
+
+__device__ __forceinline__ bool in_sorted_list(const int32_t* __restrict__ a, int64_t begin, int64_t end, int32_t v) {
+    int64_t lo = begin, hi = end;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return lo < end && a[lo] == v;
+}
+
+__global__ __launch_bounds__(kStratThreads) void strat_labels_kernel(const float* __restrict__ scores, int64_t n_items,
+                                                                    float min16, float inter16, int num_fold,
+                                                                    const int64_t* __restrict__ mask_indptr,
+                                                                    const int32_t* __restrict__ mask_indices,
+                                                                    int8_t* __restrict__ labels,
+                                                                    int32_t* __restrict__ hist) {
+    __shared__ int32_t h[kMaxFolds];
+    const int64_t u = blockIdx.x;
+    if (threadIdx.x < kMaxFolds) h[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t m0 = mask_indptr ? mask_indptr[u] : 0, m1 = mask_indptr ? mask_indptr[u + 1] : 0;
+    const float* s = scores + u * n_items;
+    int8_t* lab = labels + u * n_items;
+    for (int64_t i = threadIdx.x; i < n_items; i += kStratThreads) {
+        int lv = -1;
+        if (!in_sorted_list(mask_indices, m0, m1, (int32_t)i)) {
+            // numpy float16: every operation in float, rounded back to half
+            const float d = half_round(half_round(s[i]) - min16);
+            const float q = half_round(d / inter16);
+            lv = (int)floorf(q);
+            lv = lv < 0 ? 0 : (lv > num_fold ? num_fold : lv);  // d >= 0; the top bin is label num_fold
+            atomicAdd(&h[lv], 1);
+        }
+        lab[i] = (int8_t)lv;
+    }
+    __syncthreads();
+    if (threadIdx.x <= num_fold) hist[u * (num_fold + 1) + threadIdx.x] = h[threadIdx.x];
+}
+
+__device__ __forceinline__ uint64_t item_key(uint64_t seed, int64_t u, int64_t i) {
+    return splitmix64(seed ^ splitmix64(((uint64_t)u << 32) ^ (uint64_t)i ^ 0xA5A5A5A5ull));
+}
+
+// np.rint: round half to even
+__device__ __forceinline__ int64_t rint_even(double x) { return (int64_t)rint(x); }
+
+__global__ __launch_bounds__(kStratThreads) void strat_select_kernel(const int8_t* __restrict__ labels, int64_t n_items,
+                                                                    const int32_t* __restrict__ hist, int n_bins,
+                                                                    const int32_t* __restrict__ targets, uint64_t seed,
+                                                                    int32_t* __restrict__ out, int out_stride,
+                                                                    int32_t* __restrict__ out_count) {
+    __shared__ uint32_t dh[kMaxFolds * 256];  // per (label, 8-bit digit) counts
+    __shared__ int64_t need[kMaxFolds];       // keys still to take below the threshold being refined
+    __shared__ uint64_t prefix[kMaxFolds];    // threshold bits fixed so far
+    __shared__ uint64_t keys_sh[kMaxStratK];
+    __shared__ int32_t items_sh[kMaxStratK];
+    __shared__ int32_t n_sel;
+    const int64_t u = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int8_t* lab = labels + u * n_items;
+    // per-label quotas: K = min(target, eligible items), n_l = rint(K * hist_l / eligible)
+    const int target = min(targets[u], out_stride);
+    if (tid == 0) {
+        int64_t total = 0;
+        for (int l = 0; l < n_bins; ++l) total += hist[u * n_bins + l];
+        const int64_t K = min<int64_t>(target, total);
+        for (int l = 0; l < n_bins; ++l) {
+            need[l] = total > 0 ? rint_even((double)K * hist[u * n_bins + l] / (double)total) : 0;
+            prefix[l] = 0;
+        }
+        n_sel = 0;
+    }
+    __syncthreads();
+    // radix select, 8 passes of 8 bits from the top: after pass p, prefix[l] holds the top 8(p+1)
+    // bits of the need[l]-th smallest key of label l (need[l] counts down the keys already below it)
+    for (int pass = 0; pass < 8; ++pass) {
+        const int shift = 56 - 8 * pass;
+        for (int j = tid; j < n_bins * 256; j += kStratThreads) dh[j] = 0;
+        __syncthreads();
+        for (int64_t i = tid; i < n_items; i += kStratThreads) {
+            const int l = lab[i];
+            if (l < 0 || l >= n_bins || need[l] <= 0) continue;
+            const uint64_t k = item_key(seed, u, i);
+            const uint64_t hi_mask = pass == 0 ? 0ull : (~0ull << (shift + 8));
+            if ((k & hi_mask) != prefix[l]) continue;
+            atomicAdd(&dh[l * 256 + ((k >> shift) & 255)], 1u);
+        }
+        __syncthreads();
+        if (tid < n_bins && need[tid] > 0) {
+            int64_t acc = 0;
+            int dsel = 255;
+            for (int dgt = 0; dgt < 256; ++dgt) {
+                const int64_t c = dh[tid * 256 + dgt];
+                if (acc + c >= need[tid]) {
+                    dsel = dgt;
+                    break;
+                }
+                acc += c;
+            }
+            need[tid] -= acc;  // keys strictly below the chosen digit are taken
+            prefix[tid] |= (uint64_t)dsel << shift;
+        }
+        __syncthreads();
+    }
+    // take every key below the label's threshold, plus need[l] keys equal to it (ties: a 64-bit
+    // hash collision; taken in arrival order)
+    for (int64_t i = tid; i < n_items; i += kStratThreads) {
+        const int l = lab[i];
+        if (l < 0 || l >= n_bins) continue;
+        const uint64_t k = item_key(seed, u, i);
+        bool take = false;
+        if (k < prefix[l]) take = true;
+        else if (k == prefix[l] && need[l] > 0)  // signed: the count may go below zero under contention
+            take = (int64_t)atomicAdd((unsigned long long*)&need[l], (unsigned long long)-1) > 0;
+        if (take) {
+            const int slot = atomicAdd(&n_sel, 1);
+            if (slot < kMaxStratK) {
+                keys_sh[slot] = k;
+                items_sh[slot] = (int32_t)i;
+            }
+        }
+    }
+    __syncthreads();
+    const int n = min(n_sel, kMaxStratK);
+    // order by key: rank of each pick among all picks (n <= 1024, O(n^2 / threads))
+    __shared__ int32_t ranked[kMaxStratK];
+    for (int a = tid; a < n; a += kStratThreads) {
+        int r = 0;
+        const uint64_t ka = keys_sh[a];
+        for (int b = 0; b < n; ++b) {
+            const uint64_t kb = keys_sh[b];
+            r += (kb < ka || (kb == ka && items_sh[b] < items_sh[a])) ? 1 : 0;
+        }
+        ranked[r] = items_sh[a];
+    }
+    __syncthreads();
+    // sample_list (recommend.py:314-325): trim to K, or pad with distinct draws from the list
+    const int K = target;
+    int32_t* o = out + u * (int64_t)out_stride;
+    const int written = n >= K ? K : min(K, 2 * n);
+    for (int j = tid; j < written; j += kStratThreads) o[j] = ranked[j < n ? j : j - n];
+    if (tid == 0) out_count[u] = written;
+}
+
+}  // namespace
+}  // namespace lgx
+
+using namespace lgx;
+
+extern "C" int lgx_strat_labels(const float* scores, int64_t n_users, int64_t n_items, float min16, float inter16,
+                                int num_fold, const int64_t* mask_indptr, const int32_t* mask_indices, int8_t* labels,
+                                int32_t* hist, lgx_stream_t stream) {
+    LGX_REQUIRE(n_users >= 0 && n_items >= 0 && num_fold >= 1 && num_fold < kMaxFolds && n_items < INT32_MAX,
+                LGX_ERR_INVALID_ARG, "lgx_strat_labels: bad sizes (num_fold in [1, %d))", kMaxFolds);
+    LGX_REQUIRE(inter16 > 0.0f, LGX_ERR_INVALID_ARG, "lgx_strat_labels: inter must be > 0");
+    if (n_users == 0) return LGX_OK;
+    LGX_REQUIRE(scores && labels && hist && (!mask_indptr || mask_indices), LGX_ERR_INVALID_ARG,
+                "lgx_strat_labels: null pointer");
+    strat_labels_kernel<<<(unsigned)n_users, kStratThreads, 0, as_hip(stream)>>>(
+        scores, n_items, min16, inter16, num_fold, mask_indptr, mask_indices, labels, hist);
+    LGX_LAUNCH_CHECK();
+    return LGX_OK;
+}
+
+extern "C" int lgx_strat_select(const int8_t* labels, int64_t n_users, int64_t n_items, const int32_t* hist,
+                                int n_bins, const int32_t* targets, uint64_t seed, int32_t* out, int out_stride,
+                                int32_t* out_count, lgx_stream_t stream) {
+    LGX_REQUIRE(n_users >= 0 && n_items >= 0 && n_bins >= 1 && n_bins <= kMaxFolds && n_items < INT32_MAX,
+                LGX_ERR_INVALID_ARG, "lgx_strat_select: bad sizes (n_bins in [1, %d])", kMaxFolds);
+    LGX_REQUIRE(out_stride >= 1 && out_stride <= kMaxStratK, LGX_ERR_UNSUPPORTED,
+                "lgx_strat_select: at most %d candidates per user", kMaxStratK);
+    if (n_users == 0) return LGX_OK;
+    LGX_REQUIRE(labels && hist && targets && out && out_count, LGX_ERR_INVALID_ARG, "lgx_strat_select: null pointer");
+    strat_select_kernel<<<(unsigned)n_users, kStratThreads, 0, as_hip(stream)>>>(
+        labels, n_items, hist, n_bins, targets, seed, out, out_stride, out_count);
+    LGX_LAUNCH_CHECK();
+    return LGX_OK;
+}

@@ -152,3 +152,70 @@ def elasticity_item(mat_candidate: Dict[int, List[int]], dataset_name: str, seed
     out_dir = os.path.join(data_root, dataset_name, "rec", str(seed))
     os.makedirs(out_dir, exist_ok=True)
     np.save(os.path.join(out_dir, "rec_ela.npy"), ragged_topk(key, indptr, items, K))
+
+
+def stratification_bounds(emb_user: torch.Tensor, emb_item: torch.Tensor, num_fold: int = 10,
+                          epsilon: float = 0.1) -> Tuple[float, float]:
+    """(min_dis, inter) of recommend.py:375-378 in numpy's float16 arithmetic.  The float16 cast is
+    monotone, so the extremes of the cast matrix are the casts of the fp32 extremes (fused kernel)."""
+    mn, mx = similarity_minmax(emb_user, emb_item)
+    max_dis, min_dis = np.float16(mx) + epsilon, np.float16(mn)
+    inter = (max_dis - min_dis) / num_fold
+    return float(min_dis), float(inter)
+
+
+def stratified_candidates(emb_user: torch.Tensor, emb_item: torch.Tensor, train: Sequence[Sequence[int]],
+                          targets: Sequence[int], num_fold: int = 10, epsilon: float = 0.1, seed: int = 0,
+                          batch: int = 4096) -> List[List[int]]:
+    """Per user, the stratified candidate list of create_candidates_stratification_sub +
+    sample_list (recommend.py:314-356): labels by lgx_strat_labels over lgx_score_dense rows, the
+    per-label random picks by lgx_strat_select."""
+    from . import _lib
+    dev = emb_user.device
+    U, I = emb_user.shape[0], emb_item.shape[0]
+    min16, inter16 = stratification_bounds(emb_user, emb_item, num_fold, epsilon)
+    mp, mi = ops.lists_to_device_csr(train, dev, sort=True)
+    tgt = torch.as_tensor(np.asarray(targets, dtype=np.int32), device=dev)
+    K = int(max(1, int(tgt.max().item()) if U else 1))
+    out_lists: List[List[int]] = []
+    L = _lib.lib()
+    st = ops._stream_ptr(dev)
+    for b0 in range(0, U, batch):
+        b1 = min(U, b0 + batch)
+        S = ops.score_dense(emb_user[b0:b1].contiguous(), emb_item)
+        labels = torch.empty((b1 - b0, I), dtype=torch.int8, device=dev)
+        hist = torch.empty((b1 - b0, num_fold + 1), dtype=torch.int32, device=dev)
+        _lib.check(L.lgx_strat_labels(S.data_ptr(), b1 - b0, I, min16, inter16, num_fold, mp[b0:].data_ptr(),
+                                      mi.data_ptr(), labels.data_ptr(), hist.data_ptr(), st), "lgx_strat_labels")
+        del S
+        out = torch.empty((b1 - b0, K), dtype=torch.int32, device=dev)
+        cnt = torch.empty(b1 - b0, dtype=torch.int32, device=dev)
+        _lib.check(L.lgx_strat_select(labels.data_ptr(), b1 - b0, I, hist.data_ptr(), num_fold + 1,
+                                      tgt[b0:b1].contiguous().data_ptr(), (seed * 0x9E3779B97F4A7C15 + b0) % 2 ** 64,
+                                      out.data_ptr(), K, cnt.data_ptr(), st), "lgx_strat_select")
+        o, c = out.cpu().numpy(), cnt.cpu().numpy()
+        out_lists.extend(o[j, :c[j]].tolist() for j in range(b1 - b0))
+    return out_lists
+
+
+def create_candidates_stratification(dataset_name: str, seed: int, K_c: int = 1000, num_fold: int = 10,
+                                     epsilon: float = 0.1, data_root: str = "data", device="cuda") -> Dict[int, List[int]]:
+    """recommend.create_candidates_stratification: per user the stratified sample of K_c - |test|
+    non-train items followed by the user's test items; saved as rec/<seed>/candidate.npy (a pickled
+    dict, as np.save writes it) and returned.  The cache files are not read back (always recomputed)."""
+    import pandas as pd
+    emb_item = np.load(os.path.join(data_root, dataset_name, "emb_item.npy"), allow_pickle=False)
+    emb_user = np.load(os.path.join(data_root, dataset_name, "emb_user.npy"), allow_pickle=False)
+    eu = torch.from_numpy(np.ascontiguousarray(emb_user, dtype=np.float32)).to(device)
+    ei = torch.from_numpy(np.ascontiguousarray(emb_item, dtype=np.float32)).to(device)
+    U = eu.shape[0]
+    train = train_lists(dataset_name, U, data_root)
+    test = pd.read_csv(os.path.join(data_root, dataset_name, "rating_test.csv")) \
+        .groupby("userInd")["itemInd"].apply(list).to_dict()
+    targets = [K_c - len(test.get(u, [])) for u in range(len(train))]
+    cands = stratified_candidates(eu[:len(train)], ei, train, targets, num_fold, epsilon, seed)
+    mat_candidate = {u: c + list(test.get(u, [])) for u, c in enumerate(cands)}
+    out_dir = os.path.join(data_root, dataset_name, "rec", str(seed))
+    os.makedirs(out_dir, exist_ok=True)
+    np.save(os.path.join(out_dir, "candidate.npy"), mat_candidate)
+    return mat_candidate

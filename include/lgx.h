@@ -26,6 +26,7 @@
  *   lgx_foldout_metrics    evaluate_foldout                     LightGCN-tf/evaluator/cpp/include/evaluate_foldout.h:115-195
  *   lgx_gather_scores      accuracy_cf / elasticity_item per-user candidate dot  recommend.py:167-171, 214-217
  *   lgx_parse_lines_*      Loader / Data file parsing            code/dataloader.py:247-277; load_data.py:27-48
+ *   lgx_strat_labels/select create_candidates_stratification   recommend.py:314-452
  *   lgx_sample_bpr         sample_negative / sample_negative_ByUser   sources/sampling.cpp:27-86
  *   lgx_list_dot_reduce    difference / ser1 / ser2 / diversity per-user list products
  *                          recommend.py:305-307; utils.py:34-35, 117-121, 265-267
@@ -189,6 +190,24 @@ int lgx_foldout_metrics(const int32_t* rankings, int64_t users, int k, const int
 int lgx_gather_scores(const float* emb_user, const float* emb_item, int64_t n_users, int64_t d,
                       const int64_t* cand_indptr, const int32_t* cand_items, int64_t n_pairs,
                       float* scores, lgx_stream_t stream);
+
+/* ---------------------------------------------------------------- 8(f) rank 4: stratified candidates */
+/*
+ * recommend.create_candidates_stratification (recommend.py:359-452):
+ * lgx_strat_labels: scores [U, I] f32 (E_user . E_item^T rows) -> labels [U, I] int8 =
+ *   floor((f16(s) - min16) / inter16) in numpy's float16 arithmetic, -1 for the user's masked
+ *   (train) items (sorted CSR, optional); hist [U, num_fold + 1] int32 label counts.
+ * lgx_strat_select: per user, from every label group rint(K * |group| / |eligible|) items
+ *   uniformly at random (K = min(targets[u], eligible, out_stride)), in a seed-fixed random order,
+ *   padded / trimmed to targets[u] like sample_list -> out [U, out_stride], out_count [U];
+ *   out_stride <= 1024.
+ */
+int lgx_strat_labels(const float* scores, int64_t n_users, int64_t n_items, float min16, float inter16,
+                     int num_fold, const int64_t* mask_indptr, const int32_t* mask_indices, int8_t* labels,
+                     int32_t* hist, lgx_stream_t stream);
+int lgx_strat_select(const int8_t* labels, int64_t n_users, int64_t n_items, const int32_t* hist, int n_bins,
+                     const int32_t* targets, uint64_t seed, int32_t* out, int out_stride, int32_t* out_count,
+                     lgx_stream_t stream);
 
 /* ---------------------------------------------------------------- 8(f) rank 3: interaction files */
 /*

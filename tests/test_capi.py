@@ -83,3 +83,12 @@ def test_sampler_rejects_bad_arguments_before_device_work():
     assert L.lgx_sample_bpr(p, p, 10, 100, None, 101, 10, 1, 1, p, None) == 1
     # empty catalog
     assert L.lgx_sample_bpr(p, p, 10, 0, None, 10, 1, 1, 1, p, None) == 1
+
+
+def test_stratification_rejects_bad_arguments_before_device_work():
+    from factors_of_serendipity_recommendation_amd import _lib
+    L = _lib.lib()
+    p = ctypes.c_void_p(16)
+    assert L.lgx_strat_labels(p, 1, 10, 0.0, 0.0, 10, None, None, p, p, None) == 1  # inter must be > 0
+    assert L.lgx_strat_labels(p, 1, 10, 0.0, 0.5, 40, None, None, p, p, None) == 1  # too many folds
+    assert L.lgx_strat_select(p, 1, 10, p, 11, p, 1, p, 2048, p, None) == 3         # > 1024 per user
