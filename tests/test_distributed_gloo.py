@@ -72,7 +72,7 @@ def _worker(rank, world, port, K, result_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,K", [(2, 3), (2, 4), (3, 1), (2, 2)])
+@pytest.mark.parametrize("world,K", [(2, 3), (2, 4), (3, 1), (2, 2), (4, 3), (8, 2)])
 def test_sharded_propagation_gloo(world, K):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
