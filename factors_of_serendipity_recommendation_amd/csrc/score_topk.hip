@@ -906,9 +906,11 @@ SplitPlan plan_splits(int64_t B, int64_t n_items, int dtype, int64_t d, int k) {
         const int64_t resident = lds_resident(waves);
         const int64_t ut = ceil_div(B, users);
         const int64_t tiles = ceil_div(n_items, tile_items);
-        if (ut >= 2 * resident)  // >= 2 full rounds: no catalog split, XCD-rotated sweeps
-            return {1, tiles * tile_items, true, false, ut, waves};
-        // >= 2 rounds of resident workgroups, >= 4 tiles per split, a multiple of 8 when possible
+        // a full round or more: no catalog split -- every split repeats the list-filling phase, which
+        // costs more than a partly filled last round (which plan_ranges moves to a split launch)
+        if (ut >= resident) return {1, tiles * tile_items, true, false, ut, waves};
+        // under one round: split the catalog for >= 2 rounds of workgroups, >= 4 tiles per split,
+        // a multiple of 8 when possible
         int64_t s = ceil_div(2 * resident, ut);
         s = std::min<int64_t>(s, std::max<int64_t>(1, tiles / 4));
         s = std::max<int64_t>(1, std::min<int64_t>(s, 256));
@@ -1012,9 +1014,10 @@ int plan_ranges(int64_t B, int64_t n_items, int dtype, int64_t d, int k, UserRan
     int n = 0;
     int64_t full = B;
     const int64_t resident = lds_resident(p.waves);
-    if (p.lds && p.n_splits == 1 && p.n_utiles >= 2 * resident) {  // full-sweep mode
+    if (p.lds && p.n_splits == 1 && p.n_utiles >= resident) {  // full-sweep mode
         const int64_t rem_tiles = p.n_utiles % resident;
-        if (rem_tiles != 0 && rem_tiles < resident * 3 / 4) full = (p.n_utiles - rem_tiles) * p.waves * kUsersPerWave;
+        // measured: a 67-tile tail (of 256) runs faster as a split launch, a 135-tile one slower
+        if (rem_tiles != 0 && rem_tiles * 100 < resident * 35) full = (p.n_utiles - rem_tiles) * p.waves * kUsersPerWave;
     }
     size_t off = 0;
     r[n++] = {0, full, plan_splits(full, n_items, dtype, d, k), 0};
