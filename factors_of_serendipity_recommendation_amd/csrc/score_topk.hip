@@ -23,6 +23,7 @@
 //     sorted partial list and a one-wave-per-user merge (register bitonic network) finishes, adds
 //     the masked tail when fewer than k unmasked items exist, applies the optional sigmoid.
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 
 #include "wave_topk.h"
@@ -909,12 +910,21 @@ SplitPlan plan_splits(int64_t B, int64_t n_items, int dtype, int64_t d, int k) {
         // a full round or more: no catalog split -- every split repeats the list-filling phase, which
         // costs more than a partly filled last round (which plan_ranges moves to a split launch)
         if (ut >= resident) return {1, tiles * tile_items, true, false, ut, waves};
-        // under one round: split the catalog for >= 2 rounds of workgroups, >= 4 tiles per split,
-        // a multiple of 8 when possible
-        int64_t s = ceil_div(2 * resident, ut);
-        s = std::min<int64_t>(s, std::max<int64_t>(1, tiles / 4));
-        s = std::max<int64_t>(1, std::min<int64_t>(s, 256));
-        if (s >= 8) s = s / 8 * 8;
+        // under one round: split the catalog.  Time ~ rounds / s * f(s): each split repeats the
+        // list-filling phase, measured +18 / +25 / +31 % per doubling of s from 2 to 16, i.e.
+        // log2 f = 0.12 L + 0.04 L^2 with L = log2 s.  Take the best s among 1-7 and multiples of 8
+        // (XCD-affine), >= 4 tiles per split
+        int64_t s = 1;
+        double best = 1e300;
+        const int64_t s_max = std::max<int64_t>(1, std::min<int64_t>(256, tiles / 4));
+        for (int64_t c = 1; c <= s_max; c = c < 8 ? c + 1 : c + 8) {
+            const double L = std::log2((double)c);
+            const double t = (double)ceil_div(ut * c, resident) / (double)c * std::exp2(0.12 * L + 0.04 * L * L);
+            if (t < best - 1e-12) {
+                best = t;
+                s = c;
+            }
+        }
         const int64_t per = ceil_div(tiles, s) * tile_items;
         const int n = (int)ceil_div(n_items, per);
         return {n, per, true, n % 8 == 0, ut, waves};
