@@ -264,8 +264,8 @@ def main():
     ap.add_argument("--score-users", type=int, default=1_000_000)
     ap.add_argument("--score-items", type=int, default=1_000_000)
     ap.add_argument("--score-steps", type=int, default=2)
-    ap.add_argument("--cpu-nnz", type=int, default=6_000_000)
-    ap.add_argument("--cpu-score-users", type=int, default=2000)
+    ap.add_argument("--cpu-nnz", type=int, default=40_000_000)
+    ap.add_argument("--cpu-score-users", type=int, default=4000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scoring", action="store_true")
     ap.add_argument("--no-propagation", action="store_true", help="development: scoring leg only")

@@ -27,6 +27,16 @@ namespace {
 
 constexpr int kThreads = 256;
 
+// LGX_SPMM_NT (development builds only, tools/Makefile): stream the CSR arrays with
+// non-temporal loads so that they do not displace gathered table rows from L2 / MALL
+#ifdef LGX_SPMM_NT
+template <typename V>
+__device__ __forceinline__ V stream_load(const V* p) { return __builtin_nontemporal_load(p); }
+#else
+template <typename V>
+__device__ __forceinline__ V stream_load(const V* p) { return *p; }
+#endif
+
 template <typename T>
 struct Vec;
 template <>
@@ -170,8 +180,8 @@ __global__ __launch_bounds__(kThreads) void spmm_segments(LayerArgs a) {
 
     for (int64_t base = b; base < e; base += G) {
         const int n = (int)min((int64_t)G, e - base);
-        const int my_col = gl < n ? a.indices[base + gl] : 0;
-        const float my_val = gl < n ? a.vals[base + gl] : 0.0f;
+        const int my_col = gl < n ? stream_load(a.indices + base + gl) : 0;
+        const float my_val = gl < n ? stream_load(a.vals + base + gl) : 0.0f;
         for (int t = 0; t < n; t += UNROLL) {
             float x[UNROLL][CPL][VEC];
             float w[UNROLL];
