@@ -626,7 +626,14 @@ __device__ __forceinline__ uint32_t lds_u32(const void* p) {
 // buffer tile t-1 used (every wave left it at the barrier closing t-1), computes tile t, then
 // waits for its own pieces of tile t+1 (vmcnt leaves the younger tiles' pieces in flight) and
 // joins the barrier that publishes tile t+1 to all waves.
-template <int KSTEPS, bool MINMAX, int ABLATE = 0, int WAVES = 8, int NACC = 2>
+//
+// Stagger (STAGGER): waves w and w + WAVES/2 share a SIMD and would otherwise reach their MFMAs,
+// their top-k epilogues and the barrier in lockstep, leaving the matrix unit idle during the
+// epilogue.  The upper half of the waves runs each tile's epilogue one iteration late -- right after
+// the barrier, before the MFMAs of the next tile -- so on every SIMD one wave's epilogue (VALU, LDS,
+// mask loads) overlaps its partner's MFMAs.  The late epilogue only reads the accumulators, which
+// stay in registers across the barrier; results are bit for bit those of the unstaggered order.
+template <int KSTEPS, bool MINMAX, int ABLATE = 0, int WAVES = 8, int NACC = 2, bool STAGGER = true>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf) {
     typedef LdsGeom<KSTEPS, WAVES, NACC> G;
@@ -716,12 +723,15 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
     wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(ahead, ntiles) - 1));
     __syncthreads();
     int buf = 0, sbuf = ahead;  // buffer of tile t / of tile t + ahead
+    const bool late = STAGGER && ABLATE == 0 && wave >= WAVES / 2;  // wave-uniform
+    f32x16 acc0, acc1;  // late waves: tile t-1's scores, held across the barrier
+    int64_t prev_t0 = 0;
     for (int64_t t = 0; t < ntiles; ++t) {
         LGX_STAT_T0
         const int64_t t0 = tile_start(t);
         if (t + ahead < ntiles) stage(sbuf, tile_start(t + ahead));
+        if (late && t > 0) st.template block<MINMAX, NACC>(a, acc0, acc1, prev_t0, i_end);
         const unsigned char* T = tiles + buf * G::TILE;
-        f32x16 acc0, acc1;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             acc0[r] = 0.0f;
@@ -761,9 +771,10 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
             st.mx = fmaxf(st.mx, z);
         } else if (ABLATE == 3) {  // development: filter fast path only
             st.template block<MINMAX, NACC, true>(a, acc0, acc1, t0, i_end);
-        } else {
+        } else if (!late) {
             st.template block<MINMAX, NACC>(a, acc0, acc1, t0, i_end);
         }
+        prev_t0 = t0;
 #ifdef LGX_SCORE_STATS
         const uint64_t stat_t2_ = __builtin_amdgcn_s_memtime();
         st.stat_[4] += stat_t2_ - stat_t1_;  // top-k work
@@ -779,6 +790,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
         buf = buf + 1 == nbuf ? 0 : buf + 1;
         sbuf = sbuf + 1 == nbuf ? 0 : sbuf + 1;
     }
+    if (late && ntiles > 0) st.template block<MINMAX, NACC>(a, acc0, acc1, prev_t0, i_end);
     st.flush(a, split, lane);
 #ifdef LGX_SCORE_STATS
     { uint64_t* stat_ = st.stat_; LGX_STAT_FLUSH }
@@ -975,19 +987,27 @@ inline int lds_ring_buffers(size_t tile, size_t lists, int wg_per_cu) {
     return (int)std::max<size_t>(2, std::min<size_t>(4, fit));
 }
 
-template <int KS, bool MM, int ABL, int WAVES, int NACC>
-int launch_lds_shape(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
+template <int KS, bool MM, int ABL, int WAVES, int NACC, bool STAGGER>
+int launch_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     typedef LdsGeom<KS, WAVES, NACC> G;
     const size_t lists = (size_t)WAVES * list_bytes_per_wave(a.k);
     const int nbuf = lds_ring_buffers(G::TILE, lists, WAVES == 4 ? 2 : 1);
     const size_t shmem = (size_t)nbuf * G::TILE + lists;
-    int rc = set_lds_limit(score_topk_bf16_lds<KS, MM, ABL, WAVES, NACC>, shmem);
+    int rc = set_lds_limit(score_topk_bf16_lds<KS, MM, ABL, WAVES, NACC, STAGGER>, shmem);
     if (rc) return rc;
     const unsigned grid = (unsigned)(p.n_utiles * p.n_splits);
-    score_topk_bf16_lds<KS, MM, ABL, WAVES, NACC><<<grid, WAVES * 64, shmem, stream>>>(
+    score_topk_bf16_lds<KS, MM, ABL, WAVES, NACC, STAGGER><<<grid, WAVES * 64, shmem, stream>>>(
         a, p.xcd_affine ? 1 : 0, p.n_utiles, nbuf);
     LGX_LAUNCH_CHECK();
     return LGX_OK;
+}
+
+template <int KS, bool MM, int ABL, int WAVES, int NACC>
+int launch_lds_shape(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
+    // development switch (timing studies only): LGX_SCORE_NOSTAGGER=1 runs the lockstep order
+    static const char* ns = getenv("LGX_SCORE_NOSTAGGER");
+    if (ABL == 0 && ns && ns[0] == '1') return launch_lds_kernel<KS, MM, ABL, WAVES, NACC, false>(a, p, stream);
+    return launch_lds_kernel<KS, MM, ABL, WAVES, NACC, true>(a, p, stream);
 }
 
 template <bool MM, int ABL = 0>

@@ -24,6 +24,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--lib", default=None)
 ap.add_argument("--blocks", default="8,20")
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--hot", default="", help="hot-column set sizes to split off, e.g. 4096,16384")
 args = ap.parse_args()
 
 from factors_of_serendipity_recommendation_amd import _lib  # noqa: E402
@@ -81,6 +82,39 @@ ms = timed(lambda: ops.propagate_layer(sh.A_pull, Xi, _lib.LGX_LAYER_PLAIN, Y=Yu
 report("user rows <- item table (A_pull)", ms, layer_bytes(sh.A_pull.nnz, U, d, 2))
 ms = timed(lambda: ops.propagate_layer(sh.A_push, Xu, _lib.LGX_LAYER_PLAIN, Y=Yi), args.reps)
 report("item rows <- user table (A_push)", ms, layer_bytes(sh.A_push.nnz, I, d, 2))
+
+
+
+def split_csr(G, keep_col):
+    """(hot, cold) CSRs of G: edges whose column is / is not in keep_col (bool [n_cols])."""
+    r = torch.repeat_interleave(torch.arange(G.n_rows, device="cuda", dtype=torch.int64), torch.diff(G.indptr))
+    hot = keep_col[G.indices.to(torch.int64)]
+    outs = []
+    for sel in (hot, ~hot):
+        ip = torch.zeros(G.n_rows + 1, dtype=torch.int64, device="cuda")
+        ip[1:] = torch.cumsum(torch.bincount(r[sel], minlength=G.n_rows), 0)
+        outs.append(_planned(ip, G.indices[sel], G.vals[sel], G.n_rows, G.n_cols, None))
+    return outs
+
+
+for name, G, X, n_out in (("A_pull", sh.A_pull, Xi, U), ("A_push", sh.A_push, Xu, I)):
+    if not args.hot:
+        break
+    deg = torch.bincount(G.indices.to(torch.int64), minlength=G.n_cols)
+    order = torch.argsort(deg, descending=True)
+    outb = torch.empty((n_out, d), dtype=torch.float32, device="cuda")
+    for H in [int(x) for x in args.hot.split(",")]:
+        keep = torch.zeros(G.n_cols, dtype=torch.bool, device="cuda")
+        keep[order[:H]] = True
+        hot, cold = split_csr(G, keep)
+        torch.cuda.synchronize()
+        ms_h = timed(lambda: ops.propagate_layer(hot, X, _lib.LGX_LAYER_PARTIAL, out=outb), args.reps)
+        ms_c = timed(lambda: ops.propagate_layer(cold, X, _lib.LGX_LAYER_PARTIAL, out=outb), args.reps)
+        report(f"{name} hot {H} cols ({hot.nnz / G.nnz:.2f} of nnz)", ms_h, layer_bytes(hot.nnz, n_out, d, 2, 4))
+        report(f"{name} cold rest", ms_c, layer_bytes(cold.nnz, n_out, d, 2, 4))
+        del hot, cold
+        torch.cuda.empty_cache()
+    del outb
 
 P = sh.A_push
 rows = torch.repeat_interleave(torch.arange(P.n_rows, device="cuda", dtype=torch.int64), torch.diff(P.indptr))
