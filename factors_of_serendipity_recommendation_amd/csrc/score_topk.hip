@@ -127,13 +127,14 @@ __device__ __forceinline__ int tile_row(int r, int h) { return (r & 3) + 8 * (r 
 
 // LDS bytes of the per-wave lists: keys [32][kstride] u64 (16-B aligned rows, plus spare keys so
 // that the vectorised rescan of user 31 stays inside the allocation), then the deferred-candidate
-// slots [64 lanes][kPendSlots] u64
+// slots [64 lanes][kPendSlots + 1] u64 (the last slot of a lane takes the branch-free event path's
+// writes once its real slots are full)
 __host__ __device__ constexpr int kstride(int k) { return (k + 1) & ~1; }
 constexpr int kListSpare = 8;  // the 8-key rescan of user 31 may read past its row
 constexpr int kPendSlots = 4;
 __host__ __device__ constexpr size_t list_keys_per_wave(int k) { return (size_t)kUsersPerWave * kstride(k) + kListSpare; }
 __host__ __device__ constexpr size_t list_bytes_per_wave(int k) {
-    return (list_keys_per_wave(k) + 64 * kPendSlots) * 8;
+    return (list_keys_per_wave(k) + 64 * (kPendSlots + 1)) * 8;
 }
 
 // value held by lane (lane ^ 32): one v_permlane32_swap, no LDS traffic
@@ -160,7 +161,8 @@ struct WaveTopK {
     static constexpr int kPend = kPendSlots;
     static_assert(kPend == 4, "drop_masked's lockstep search is written for 4 slots");
     LGX_STAT_DECL
-    uint64_t* pend;  // this lane's kPend slots in LDS
+    // this lane's kPend (+1 scratch) slots in LDS; a slot holds the raw pair (score bits, item << 32)
+    uint64_t* pend;
     int pcnt;
     float tau;       // filter threshold: -inf until the list is full, +inf for padding users
     int32_t tau_i;
@@ -221,7 +223,7 @@ struct WaveTopK {
         len = 0;
         mp = 0;
         kmin = 0;
-        pend = pend_w + lane * kPend;
+        pend = pend_w + lane * (kPend + 1);
         pcnt = 0;
         tau = ok ? -INFINITY : INFINITY;  // padding users never produce candidates
         tau_i = 0x7fffffff;
@@ -257,17 +259,22 @@ struct WaveTopK {
     // consume NACC (1 or 2) 32-item accumulator tiles; tile j's item rows start at i0 + 32 j
     // (items >= i_end ignored).  Fast path: a max tree and ONE compare per lane against tau,
     // OR-ed into a wave-wide flag.  Rows past i_end (tail block only) are set to -inf first.
-    template <bool MINMAX, int NACC, bool FASTONLY = false>
+    // L16: the scores come from the 16x16x32 main loop after its lane exchange (exchange16): lane
+    // half h holds items 16 q + 8 h + (r & 7) of 16-item block q = 2 j + (r >> 3); otherwise the
+    // 32x32x16 accumulator layout, items 32 j + (r & 3) + 8 (r >> 2) + 4 h
+    // TAIL: the block may run past i_end (callers that know it does not pass false, so that the
+    // common path never rewrites the accumulators and the compiler keeps them where they are)
+    template <bool MINMAX, int NACC, bool FASTONLY = false, bool L16 = false, bool TAIL = true>
     __device__ __forceinline__ void block(const ScoreArgs& a, f32x16 acc0, f32x16 acc1, int64_t i0, int64_t i_end) {
-        const int64_t ib = i0 + 4 * h;  // item of accumulator row 0 of this lane half
-        const bool tail = i0 + 32 * NACC > i_end;
+        const int64_t ib = i0 + (L16 ? 8 : 4) * h;  // item of accumulator row 0 of this lane half
+        const bool tail = TAIL && i0 + 32 * NACC > i_end;
         const int64_t rem64 = i_end - ib;
         const int32_t rem = rem64 > (1 << 30) ? (1 << 30) : (int32_t)rem64;  // offsets < rem are items
         if (tail) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                if (row_off(0, r) >= rem) acc0[r] = -INFINITY;
-                if (NACC == 2 && row_off(1, r) >= rem) acc1[r] = -INFINITY;
+                if (row_off<L16>(0, r) >= rem) acc0[r] = -INFINITY;
+                if (NACC == 2 && row_off<L16>(1, r) >= rem) acc1[r] = -INFINITY;
             }
         }
         // maxima of the 8-score groups {acc0 rows 0-7, 8-15, acc1 rows 0-7, 8-15}: the fast-path
@@ -301,53 +308,59 @@ struct WaveTopK {
 #ifdef LGX_SCORE_STATS
         const uint64_t ev_t0 = __builtin_amdgcn_s_memtime();
 #endif
-        slow<NACC>(a, acc0, acc1, g, ib, rem);
+        slow<NACC, L16>(a, acc0, acc1, g, ib, rem);
 #ifdef LGX_SCORE_STATS
         stat_[7] += __builtin_amdgcn_s_memtime() - ev_t0;
 #endif
     }
 
-    __device__ __forceinline__ static int32_t row_off(int j, int r) { return 32 * j + (r & 3) + 8 * (r >> 2); }
-
-    template <int NACC>
-    __device__ __forceinline__ void slow(const ScoreArgs& a, const f32x16& acc0, const f32x16& acc1, const float* g,
-                                         int64_t ib, int32_t rem) {
-        if (__ballot(len < k) != 0ull) {  // a list is still filling (first block): exact inserts
-            LGX_STAT(3, 1);
-            drain(a);
-            insert_now<NACC>(a, acc0, acc1, ib, survivors<NACC>(acc0, acc1, ib, rem));
-            return;
-        }
-        // every list is full: defer each survivor into this lane's slots.  One compare per score,
-        // the exact index tie-break only inside the (rarely taken) branch
-        const int64_t l64 = (int64_t)tau_i - ib;
-        const int32_t lim = l64 > (1 << 30) ? (1 << 30) : l64 < -1 ? -1 : (int32_t)l64;
-        uint32_t ovf = 0;
-#pragma unroll
-        for (int q = 0; q < 2 * NACC; ++q) {
-            if (__ballot(g[q] >= tau) == 0ull) continue;  // no lane has a survivor in this group
-#pragma unroll
-            for (int rr = 0; rr < 8; ++rr) {
-                const int j = q >> 1, r = (q & 1) * 8 + rr;
-                const float sc = j ? acc1[r] : acc0[r];
-                if (sc >= tau) {
-                    const int32_t off = row_off(j, r);
-                    if (sc > tau || off < lim) {
-                        if (pcnt < kPend) pend[pcnt++] = make_key(sc, (int32_t)ib + off);
-                        else ovf |= 1u << (16 * j + r);
-                    }
-                }
-            }
-        }
-        if (__ballot(ovf != 0u) != 0ull) {  // slots full: drain, then insert the rest exactly
-            LGX_STAT(2, 1);
-            drain(a);
-            insert_now<NACC>(a, acc0, acc1, ib, ovf & survivors<NACC>(acc0, acc1, ib, rem));
-        }
+    template <bool L16 = false>
+    __device__ __forceinline__ static int32_t row_off(int j, int r) {
+        return L16 ? 32 * j + 16 * (r >> 3) + (r & 7) : 32 * j + (r & 3) + 8 * (r >> 2);
     }
 
+    __device__ __forceinline__ static int32_t pend_item(uint64_t v) { return (int32_t)(v >> 32); }
+    __device__ __forceinline__ static uint64_t pend_key(uint64_t v) {
+        return make_key(__uint_as_float((uint32_t)v), pend_item(v));
+    }
+
+    template <int NACC, bool L16>
+    __device__ __forceinline__ void slow(const ScoreArgs& a, const f32x16& acc0, const f32x16& acc1, const float* g,
+                                         int64_t ib, int32_t rem) {
+        // Every list full: each score >= tau of a group some lane flagged is appended to this lane's
+        // deferred slots without branching -- an unconditional 8-B LDS write to slot min(n, kPend)
+        // and n += (score >= tau) -- so an event costs a few instructions per score whatever the
+        // lanes do.  Ties at tau and masked items are sorted out when the slots are drained (exact
+        // key compare, mask test).  A lane that runs past its slots (n > kPend) sends the whole
+        // block down the exact path instead: drain, then insert every survivor directly.  A list
+        // still filling (first block) takes that path too.
+        if (__ballot(len < k) == 0ull) {
+            int n = pcnt;
+#pragma unroll
+            for (int q = 0; q < 2 * NACC; ++q) {
+                if (__ballot(g[q] >= tau) == 0ull) continue;  // no lane has a survivor in this group
+#pragma unroll
+                for (int rr = 0; rr < 8; ++rr) {
+                    const int j = q >> 1, r = (q & 1) * 8 + rr;
+                    const float sc = j ? acc1[r] : acc0[r];
+                    const uint32_t item = (uint32_t)((int32_t)ib + row_off<L16>(j, r));
+                    pend[min(n, kPend)] = ((uint64_t)item << 32) | __float_as_uint(sc);
+                    n += sc >= tau ? 1 : 0;
+                }
+            }
+            if (__ballot(n > kPend) == 0ull) {
+                pcnt = n;
+                return;
+            }
+            LGX_STAT(2, 1);
+        }
+        drain(a);
+        insert_now<NACC, L16>(a, acc0, acc1, ib, survivors<NACC, L16>(acc0, acc1, ib, rem));
+    }
+
+    template <bool L16>
     __device__ __forceinline__ int32_t item_of(int64_t ib, int r) const {
-        return (int32_t)ib + row_off(r >> 4, r & 15);
+        return (int32_t)ib + row_off<L16>(r >> 4, r & 15);
     }
     template <int NACC>
     __device__ __forceinline__ static float pick(const f32x16& acc0, const f32x16& acc1, int r) {
@@ -363,7 +376,7 @@ struct WaveTopK {
     }
     // exact survivors of a block against the current list (bounds, index tie-break), branch-free;
     // item tests are relative to the lane's first item so the per-score offsets are constants
-    template <int NACC>
+    template <int NACC, bool L16>
     __device__ __forceinline__ uint32_t survivors(const f32x16& acc0, const f32x16& acc1, int64_t ib,
                                                   int32_t rem) const {
         const bool notfull = len < k;
@@ -375,7 +388,7 @@ struct WaveTopK {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const float sc = j ? acc1[r] : acc0[r];
-                const int32_t off = row_off(j, r);
+                const int32_t off = row_off<L16>(j, r);
                 const bool beats = notfull | (sc > tau) | ((sc == tau) & (off < lim));
                 cmask |= (user_ok & (off < rem) & beats) ? (1u << (16 * j + r)) : 0u;
             }
@@ -409,7 +422,7 @@ struct WaveTopK {
         uint32_t need = 0;
 #pragma unroll
         for (int j = 0; j < kPend; ++j) {
-            it[j] = j < pcnt ? key_index(pend[j]) : 0;
+            it[j] = j < pcnt ? pend_item(pend[j]) : 0;
             if (j < pcnt && bloom_test(bloom_h1(it[j])) && bloom_test(bloom_h2(it[j]))) need |= 1u << j;
         }
         if (__ballot(need != 0u) == 0ull) return keep;
@@ -471,7 +484,7 @@ struct WaveTopK {
             if (__ballot(ph == h && pcnt > 0) == 0ull) continue;
             if (ph == h) {
                 for (int j = 0; j < pcnt; ++j)
-                    if ((keep >> j) & 1u) insert_key<false>(a, pend[j]);
+                    if ((keep >> j) & 1u) insert_key<false>(a, pend_key(pend[j]));
             }
             sync_from(ph);
         }
@@ -479,7 +492,7 @@ struct WaveTopK {
         refresh_tau();
     }
     // insert a block's survivors directly (pending list already drained)
-    template <int NACC>
+    template <int NACC, bool L16>
     __device__ __forceinline__ void insert_now(const ScoreArgs& a, const f32x16& acc0, const f32x16& acc1, int64_t ib,
                                                uint32_t cmask) {
         for (int ph = 0; ph < 2; ++ph) {
@@ -489,7 +502,7 @@ struct WaveTopK {
                 while (todo) {  // one copy of the insertion code, one iteration per survivor
                     const int r = __builtin_ctz(todo);
                     todo &= todo - 1;
-                    insert_key<true>(a, make_key(pick<NACC>(acc0, acc1, r), item_of(ib, r)));
+                    insert_key<true>(a, make_key(pick<NACC>(acc0, acc1, r), item_of<L16>(ib, r)));
                 }
             }
             sync_from(ph);
@@ -633,9 +646,17 @@ __device__ __forceinline__ uint32_t lds_u32(const void* p) {
 // the barrier, before the MFMAs of the next tile -- so on every SIMD one wave's epilogue (VALU, LDS,
 // mask loads) overlaps its partner's MFMAs.  The late epilogue only reads the accumulators, which
 // stay in registers across the barrier; results are bit for bit those of the unstaggered order.
-template <int KSTEPS, bool MINMAX, int ABLATE = 0, int WAVES = 8, int NACC = 2, bool STAGGER = true>
+//
+// MFMA shape (M16): v_mfma_f32_16x16x32_bf16 holds a higher clock than 32x32x16 on random operands
+// (tools/mfma_peak: 1962 vs 1615 TF/s bare, same FLOPs per cycle).  A wave's 32 users are two
+// 16-user B blocks and its 64-item tile four 16-item A blocks: 8 accumulators of 4 scores.  One
+// v_permlane16_swap per accumulator register then regroups them so that lane l holds 32 scores of
+// user l & 31 (items 16 q + 8 h + 0..7 of block q), the layout the top-k state expects: lanes l and
+// l + 32 still share a user.
+template <int KSTEPS, bool MINMAX, int ABLATE = 0, int WAVES = 8, int NACC = 2, bool STAGGER = true, bool M16 = true>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf) {
+    static_assert(!M16 || (NACC == 2 && KSTEPS % 2 == 0), "16x16x32 path: 64-item tiles, d a multiple of 32");
     typedef LdsGeom<KSTEPS, WAVES, NACC> G;
     typedef Frag<LGX_DTYPE_BF16> F;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -663,10 +684,23 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
 
     const int64_t b = utile * G::USERS + wave * kUsersPerWave + col;
     const bool user_ok = b < a.B;
-    const int64_t qrow = user_ok ? (a.user_rows ? a.user_rows[b] : b) : 0;
     typename F::chunk uf[KSTEPS];
+    const int r16 = lane & 15, q4 = lane >> 4;
+    if (M16) {  // B fragment (ub, s) at uf[ub * KSTEPS / 2 + s]: user 16 ub + r16, features 32 s + 8 q4
 #pragma unroll
-    for (int c = 0; c < KSTEPS; ++c) uf[c] = F::load(a.Q, qrow, a.d, c, h, user_ok);
+        for (int ub = 0; ub < 2; ++ub) {
+            const int64_t bu = utile * G::USERS + wave * kUsersPerWave + 16 * ub + r16;
+            const bool ok = bu < a.B;
+            const int64_t qr = ok ? (a.user_rows ? a.user_rows[bu] : bu) : 0;
+#pragma unroll
+            for (int s2 = 0; s2 < KSTEPS / 2; ++s2)
+                uf[ub * (KSTEPS / 2) + s2] = F::load(a.Q, qr, a.d, 2 * s2 + (q4 >> 1), q4 & 1, ok);
+        }
+    } else {
+        const int64_t qrow = user_ok ? (a.user_rows ? a.user_rows[b] : b) : 0;
+#pragma unroll
+        for (int c = 0; c < KSTEPS; ++c) uf[c] = F::load(a.Q, qrow, a.d, c, h, user_ok);
+    }
     WaveTopK st;
     st.init(lk, lk + list_keys_per_wave(k), k, lane, b, user_ok);
     st.build_bloom(a);
@@ -726,12 +760,67 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
     const bool late = STAGGER && ABLATE == 0 && wave >= WAVES / 2;  // wave-uniform
     f32x16 acc0, acc1;  // late waves: tile t-1's scores, held across the barrier
     int64_t prev_t0 = 0;
-    for (int64_t t = 0; t < ntiles; ++t) {
-        LGX_STAT_T0
-        const int64_t t0 = tile_start(t);
-        if (t + ahead < ntiles) stage(sbuf, tile_start(t + ahead));
-        if (late && t > 0) st.template block<MINMAX, NACC>(a, acc0, acc1, prev_t0, i_end);
+    // scores of the tile in ring buffer `buf` into acc0 / acc1 (the same code for both wave kinds)
+    auto compute = [&]() {
         const unsigned char* T = tiles + buf * G::TILE;
+        if constexpr (M16) {
+            constexpr int KS2 = KSTEPS / 2;
+            typedef float f32x4 __attribute__((ext_vector_type(4)));
+            f32x4 c[2][4];
+#pragma unroll
+            for (int ub = 0; ub < 2; ++ub)
+#pragma unroll
+                for (int ib = 0; ib < 4; ++ib) c[ub][ib] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            // A fragment (s, ib): item 16 ib + r16, source chunk 4 s + q4 (LDS chunk ^ row swizzle)
+            const unsigned char* rowp = T + r16 * G::RB;
+            auto frag = [&](int s2, int ib) {
+                return *reinterpret_cast<const uint4*>(rowp + ib * 16 * G::RB + (((4 * s2 + q4) ^ (r16 & G::SWZ)) * 16));
+            };
+            // one fragment register per item block: its next k-step is read right after the two
+            // MFMAs that consume it, so every read has the following 6 MFMAs to land
+            uint4 fa[4];
+#pragma unroll
+            for (int ib = 0; ib < 4; ++ib) fa[ib] = frag(0, ib);
+#pragma unroll
+            for (int s2 = 0; s2 < KS2; ++s2) {
+#pragma unroll
+                for (int ib = 0; ib < 4; ++ib) {
+#pragma unroll
+                    for (int ub = 0; ub < 2; ++ub)
+                        c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            __builtin_bit_cast(bf16x8, fa[ib]), __builtin_bit_cast(bf16x8, uf[ub * KS2 + s2]),
+                            c[ub][ib], 0, 0, 0);
+                    if (s2 + 1 < KS2) fa[ib] = frag(s2 + 1, ib);
+                }
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+            for (int s2 = 0; s2 < KS2; ++s2) {
+#pragma unroll
+                for (int ib = 0; ib < 4; ++ib) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                    if (s2 + 1 < KS2) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
+            }
+            // regroup: swap(X = user block 0, Y = user block 1) between rows 2m and 2m+1 (lanes l, l^16)
+            // leaves X' = items 16 ib + 8 h + reg, Y' = items 16 ib + 8 h + 4 + reg of user l & 31
+#pragma unroll
+            for (int ib = 0; ib < 4; ++ib) {
+#pragma unroll
+                for (int reg = 0; reg < 4; ++reg) {
+                    const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(c[0][ib][reg]),
+                                                                     __float_as_uint(c[1][ib][reg]), false, false);
+                    const int r = 8 * (ib & 1) + reg;
+                    if (ib < 2) {
+                        acc0[r] = __uint_as_float(sw[0]);
+                        acc0[r + 4] = __uint_as_float(sw[1]);
+                    } else {
+                        acc1[r] = __uint_as_float(sw[0]);
+                        acc1[r + 4] = __uint_as_float(sw[1]);
+                    }
+                }
+            }
+        } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             acc0[r] = 0.0f;
@@ -764,15 +853,31 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
             if (c + 1 < KSTEPS) __builtin_amdgcn_sched_group_barrier(0x100, NACC, 0);
             __builtin_amdgcn_sched_group_barrier(0x008, NACC, 0);
         }
+        }
+    };
+    for (int64_t t = 0; t < ntiles; ++t) {
+        LGX_STAT_T0
+        const int64_t t0 = tile_start(t);
+        if (t + ahead < ntiles) stage(sbuf, tile_start(t + ahead));
+        // the split's last tile is the only one that can run past i_end: a block variant of its own
+        auto epilogue = [&](int64_t e0) {
+            if (e0 + G::TILE_ITEMS > i_end) st.template block<MINMAX, NACC, false, M16, true>(a, acc0, acc1, e0, i_end);
+            else st.template block<MINMAX, NACC, false, M16, false>(a, acc0, acc1, e0, i_end);
+        };
+        if (late && t > 0) epilogue(prev_t0);
+        compute();
+#ifdef LGX_SCORE_STATS
+        const uint64_t stat_t1_ = __builtin_amdgcn_s_memtime();
+#endif
         if (ABLATE == 1) {  // development: MFMA + LDS pipeline only (keeps the accumulators live)
             float z = 0.0f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) z += acc0[r] + (NACC == 2 ? acc1[r] : 0.0f);
             st.mx = fmaxf(st.mx, z);
         } else if (ABLATE == 3) {  // development: filter fast path only
-            st.template block<MINMAX, NACC, true>(a, acc0, acc1, t0, i_end);
+            st.template block<MINMAX, NACC, true, M16>(a, acc0, acc1, t0, i_end);
         } else if (!late) {
-            st.template block<MINMAX, NACC>(a, acc0, acc1, t0, i_end);
+            epilogue(t0);
         }
         prev_t0 = t0;
 #ifdef LGX_SCORE_STATS
@@ -790,7 +895,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
         buf = buf + 1 == nbuf ? 0 : buf + 1;
         sbuf = sbuf + 1 == nbuf ? 0 : sbuf + 1;
     }
-    if (late && ntiles > 0) st.template block<MINMAX, NACC>(a, acc0, acc1, prev_t0, i_end);
+    if (late && ntiles > 0) st.template block<MINMAX, NACC, false, M16>(a, acc0, acc1, prev_t0, i_end);
     st.flush(a, split, lane);
 #ifdef LGX_SCORE_STATS
     { uint64_t* stat_ = st.stat_; LGX_STAT_FLUSH }
@@ -987,16 +1092,16 @@ inline int lds_ring_buffers(size_t tile, size_t lists, int wg_per_cu) {
     return (int)std::max<size_t>(2, std::min<size_t>(4, fit));
 }
 
-template <int KS, bool MM, int ABL, int WAVES, int NACC, bool STAGGER>
+template <int KS, bool MM, int ABL, int WAVES, int NACC, bool STAGGER, bool M16>
 int launch_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     typedef LdsGeom<KS, WAVES, NACC> G;
     const size_t lists = (size_t)WAVES * list_bytes_per_wave(a.k);
     const int nbuf = lds_ring_buffers(G::TILE, lists, WAVES == 4 ? 2 : 1);
     const size_t shmem = (size_t)nbuf * G::TILE + lists;
-    int rc = set_lds_limit(score_topk_bf16_lds<KS, MM, ABL, WAVES, NACC, STAGGER>, shmem);
+    int rc = set_lds_limit(score_topk_bf16_lds<KS, MM, ABL, WAVES, NACC, STAGGER, M16>, shmem);
     if (rc) return rc;
     const unsigned grid = (unsigned)(p.n_utiles * p.n_splits);
-    score_topk_bf16_lds<KS, MM, ABL, WAVES, NACC, STAGGER><<<grid, WAVES * 64, shmem, stream>>>(
+    score_topk_bf16_lds<KS, MM, ABL, WAVES, NACC, STAGGER, M16><<<grid, WAVES * 64, shmem, stream>>>(
         a, p.xcd_affine ? 1 : 0, p.n_utiles, nbuf);
     LGX_LAUNCH_CHECK();
     return LGX_OK;
@@ -1004,15 +1109,27 @@ int launch_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream
 
 template <int KS, bool MM, int ABL, int WAVES, int NACC>
 int launch_lds_shape(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
-    // development switch (timing studies only): LGX_SCORE_NOSTAGGER=1 runs the lockstep order
+    // development switches (timing studies only): LGX_SCORE_NOSTAGGER=1 runs the lockstep order,
+    // LGX_SCORE_MFMA32=1 the 32x32x16 main loop
     static const char* ns = getenv("LGX_SCORE_NOSTAGGER");
-    if (ABL == 0 && ns && ns[0] == '1') return launch_lds_kernel<KS, MM, ABL, WAVES, NACC, false>(a, p, stream);
-    return launch_lds_kernel<KS, MM, ABL, WAVES, NACC, true>(a, p, stream);
+    static const char* m32 = getenv("LGX_SCORE_MFMA32");
+    if constexpr (ABL == 0 && KS == 16) {  // d = 256 (the C5 shape) only: keeps the build short
+        if (m32 && m32[0] == '1') return launch_lds_kernel<KS, MM, ABL, WAVES, NACC, true, false>(a, p, stream);
+        if (ns && ns[0] == '1') return launch_lds_kernel<KS, MM, ABL, WAVES, NACC, false, true>(a, p, stream);
+    }
+    return launch_lds_kernel<KS, MM, ABL, WAVES, NACC, true, true>(a, p, stream);
 }
 
 template <bool MM, int ABL = 0>
 int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     const int ksteps = (int)(a.d / 16);
+    if constexpr (ABL != 0) {  // development ablations: d = 256 only
+        if (ksteps != 16) {
+            set_error("lgx_score_topk: ablation builds exist for d=256 only");
+            return LGX_ERR_UNSUPPORTED;
+        }
+        return launch_lds_shape<16, MM, ABL, 8, 2>(a, p, stream);
+    }
 #define LGX_SL(KS) return launch_lds_shape<KS, MM, ABL, 8, 2>(a, p, stream)
     switch (ksteps) {
         case 2: LGX_SL(2);

@@ -6,6 +6,10 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from factors_of_serendipity_recommendation_amd import _lib  # noqa: E402
+
+if os.environ.get("LGX_LIB"):  # A/B against another build of the library on the same box
+    _lib.LIB_PATH = os.path.abspath(os.environ["LGX_LIB"])
 import factors_of_serendipity_recommendation_amd as lgx  # noqa: E402
 from factors_of_serendipity_recommendation_amd import ops  # noqa: E402
 
@@ -25,7 +29,8 @@ def run(B, n_items=1_000_000, d=256, k=20, masked=True, reps=3):
     torch.cuda.synchronize()
     t = (time.perf_counter() - t0) / reps
     tf = 2 * B * n_items * d / t / 1e12
-    print(f"B={B} masked={masked} ablate={os.environ.get('LGX_SCORE_ABLATE', '0')}: {t * 1e3:.1f} ms  {tf:.0f} TF/s",
+    tag = os.path.basename(os.environ.get("LGX_LIB", "liblgx.so"))
+    print(f"{tag} B={B} masked={masked} ablate={os.environ.get('LGX_SCORE_ABLATE', '0')}: {t * 1e3:.1f} ms  {tf:.0f} TF/s",
           flush=True)
 
 
