@@ -171,7 +171,12 @@ def bench_propagation(args, rank, world):
                      "frac": achieved / HBM_PEAK, "traffic": traffic, "traffic_unit": "GB/launch",
                      "traffic_source": traffic_src,
                      "kernel": "spmm_segments (+spmm_fixup)", "bytes_per_launch": int(bytes_per_launch),
-                     "mean_launch_ms": mean_launch_s * 1e3},
+                     "mean_launch_ms": mean_launch_s * 1e3,
+                     # achieved counts every gathered row as an HBM read, so the caches that serve part
+                     # of them can lift frac above 1; the PMC bytes over the same launch time are the
+                     # HBM rate the kernel really pulls
+                     "traffic_rate_gbs": traffic / mean_launch_s if traffic else None,
+                     "traffic_frac": traffic * 1e9 / mean_launch_s / HBM_PEAK if traffic else None},
         "graph": A if world == 1 else None, "E0": E0 if world == 1 else None,
     }
     return res

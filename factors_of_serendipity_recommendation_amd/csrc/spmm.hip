@@ -43,6 +43,10 @@ template <>
 struct Vec<float> {
     static constexpr int N = 4;
     typedef float4 raw;
+    __device__ static __forceinline__ raw load_raw(const float* p) { return *reinterpret_cast<const float4*>(p); }
+    __device__ static __forceinline__ void unpack(const raw& x, float (&v)[4]) {
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+    }
     __device__ static __forceinline__ void load(const float* p, float (&v)[4]) {
         const float4 x = *reinterpret_cast<const float4*>(p);
         v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
@@ -54,6 +58,16 @@ struct Vec<float> {
 template <>
 struct Vec<uint16_t> {
     static constexpr int N = 8;
+    typedef uint4 raw;
+    __device__ static __forceinline__ raw load_raw(const uint16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+    __device__ static __forceinline__ void unpack(const raw& x, float (&v)[8]) {
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            v[2 * j] = __uint_as_float(w[j] << 16);
+            v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+        }
+    }
     __device__ static __forceinline__ void load(const uint16_t* p, float (&v)[8]) {
         const uint4 x = *reinterpret_cast<const uint4*>(p);
         const uint32_t w[4] = {x.x, x.y, x.z, x.w};
@@ -183,7 +197,9 @@ __global__ __launch_bounds__(kThreads) void spmm_segments(LayerArgs a) {
         const int my_col = gl < n ? stream_load(a.indices + base + gl) : 0;
         const float my_val = gl < n ? stream_load(a.vals + base + gl) : 0.0f;
         for (int t = 0; t < n; t += UNROLL) {
-            float x[UNROLL][CPL][VEC];
+            // the gathered chunks stay packed (bf16: 4 VGPRs per 16 B, not 8) until their FMAs,
+            // so more of them fit in flight per wave
+            typename Vec<T>::raw x[UNROLL][CPL];
             float w[UNROLL];
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u) {
@@ -194,20 +210,19 @@ __global__ __launch_bounds__(kThreads) void spmm_segments(LayerArgs a) {
 #pragma unroll
                 for (int c = 0; c < CPL; ++c) {
                     const int64_t off = (int64_t)(c * G + gl) * VEC;
-                    if (src < n && off < d) {
-                        Vec<T>::load(xr + off, x[u][c]);
-                    } else {
-#pragma unroll
-                        for (int j = 0; j < VEC; ++j) x[u][c][j] = 0.0f;
-                    }
+                    if (src < n && off < d) x[u][c] = Vec<T>::load_raw(xr + off);
+                    else x[u][c] = typename Vec<T>::raw{};
                 }
             }
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
-                for (int c = 0; c < CPL; ++c)
+                for (int c = 0; c < CPL; ++c) {
+                    float v[VEC];
+                    Vec<T>::unpack(x[u][c], v);
 #pragma unroll
-                    for (int j = 0; j < VEC; ++j) acc[c][j] = fmaf(w[u], x[u][c][j], acc[c][j]);
+                    for (int j = 0; j < VEC; ++j) acc[c][j] = fmaf(w[u], v[j], acc[c][j]);
+                }
         }
     }
 
@@ -254,9 +269,10 @@ __global__ __launch_bounds__(kThreads) void spmm_fixup(LayerArgs a) {
     }
 }
 
-template <typename T, int G, int CPL>
+// gathers in flight per lane: a 16-lane group (d=128 bf16 / d=64 f32) issues all 16 rows of a
+// CSR chunk at once -- 29.9 vs 31.2 ms per C4 layer against 8 (tools/spmm_probe.py, same box)
+template <typename T, int G, int CPL, int UNROLL = (CPL == 1 ? (G == 16 ? 16 : 8) : (CPL == 2 ? 4 : 2))>
 int launch_layer(const LayerArgs& a, hipStream_t stream) {
-    constexpr int UNROLL = CPL == 1 ? 8 : (CPL == 2 ? 4 : 2);
     constexpr int groups_per_block = kThreads / G;
     if (a.n_segs > 0) {
         const int64_t blocks = ceil_div(a.n_segs, groups_per_block);

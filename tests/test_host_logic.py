@@ -46,10 +46,30 @@ def test_make_plan_covers_every_nonzero_once(seg_len):
     assert np.all(np.diff(lens[plan.seg_row]) <= 0)
 
 
+@pytest.mark.parametrize("seg_len", [1, 7, 64])
+def test_make_plan_phases(seg_len):
+    """phase-ordered plans (items first, then users): every nonzero once, phases contiguous in
+    launch order, longest-first inside each phase; a non-partition is rejected"""
+    rng = np.random.default_rng(100 + seg_len)
+    lens = rng.zipf(1.5, 300) % 2000
+    lens[::13] = 0
+    indptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    U = 180
+    plan = make_plan(indptr, seg_len, phases=[(U, 300), (0, U)])
+    _check_plan(indptr, plan)
+    first_user = int(np.argmax(plan.seg_row < U))
+    assert np.all(plan.seg_row[:first_user] >= U) and np.all(plan.seg_row[first_user:] < U)
+    for sl in (slice(0, first_user), slice(first_user, None)):
+        assert np.all(np.diff(lens[plan.seg_row[sl]]) <= 0)
+    with pytest.raises(ValueError):
+        make_plan(indptr, seg_len, phases=[(0, U), (U + 1, 300)])
+
+
 def test_choose_seg_len_range():
     assert choose_seg_len(0) == 64
     assert choose_seg_len(2_000_000) == 64
-    assert choose_seg_len(1_000_000_000) == 2048
+    assert choose_seg_len(1_000_000_000) == 8192
+    assert choose_seg_len(100_000_000) == 2048
 
 
 def test_balanced_bounds():
