@@ -1,0 +1,339 @@
+"""Per-row measurement of the SURVEY §8 rows that bench.py does not time (a2, a6, a9, a10, a12 and
+the §8(f) rows), each on MI355X against the roofline that bounds it, with the reference's CPU
+procedure timed beside it on a bounded sample.  Development / reporting tool, run on the GPU box:
+
+  python tools/bench_rows.py [--out gpurun_out/rows.json] [--only a2,a6]
+
+One JSON object per row.  GPU times are the median of --reps launches bracketed by HIP events on
+the stream the ops run on (torch's current stream); inputs are resident in HBM before timing.
+Algorithmic bytes / flops per row are stated next to each row in DESIGN.md §5.
+The CPU legs use oracle/ (test infrastructure) or the library calls the reference itself makes
+(torch / numpy); ``cores`` is the thread count they ran with.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import factors_of_serendipity_recommendation_amd as lgx  # noqa: E402
+from factors_of_serendipity_recommendation_amd import _lib, ops, recommend, sampling  # noqa: E402
+from factors_of_serendipity_recommendation_amd.synth import CONFIGS, synth_edges  # noqa: E402
+from oracle import oracle  # noqa: E402  (CPU legs only)
+
+HBM_PEAK = 8.0e12
+BF16_PEAK = 2.5e15
+F32_PEAK = 157.3e12
+DEV = "cuda"
+CPU_THREADS = 16
+
+
+def gpu_ms(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return float(np.median(ts))
+
+
+def cpu_s(fn):
+    t0 = time.perf_counter()
+    fn()
+    return time.perf_counter() - t0
+
+
+def emit(rows, row, gpu_ms_, units, unit, bound, algo, cpu_units, cpu_seconds, cpu_sample, cpu_cores, note=""):
+    """algo: algorithmic bytes (bound hbm) or flops (bound mfma/mfma_f32) per launch"""
+    t = gpu_ms_ / 1e3
+    peak = {"hbm": HBM_PEAK, "mfma": BF16_PEAK, "mfma_f32": F32_PEAK}[bound]
+    r = {"row": row, "gpu_ms": gpu_ms_, "value": units / t, "unit": unit,
+         "roofline": {"bound": "hbm" if bound == "hbm" else "mfma",
+                      "dtype": {"hbm": None, "mfma": "bf16", "mfma_f32": "f32"}[bound],
+                      "achieved": algo / t / (1e9 if bound == "hbm" else 1e12),
+                      "peak": peak / (1e9 if bound == "hbm" else 1e12),
+                      "unit": "GB/s" if bound == "hbm" else "TFLOP/s", "frac": algo / t / peak,
+                      "algorithmic_per_launch": algo},
+         "cpu_baseline": {"value": cpu_units / cpu_seconds if cpu_seconds else None, "unit": unit,
+                          "cores": cpu_cores, "sample": cpu_sample, "seconds": cpu_seconds},
+         "note": note}
+    r["speedup_vs_cpu"] = r["value"] / r["cpu_baseline"]["value"] if r["cpu_baseline"]["value"] else None
+    print(json.dumps(r), flush=True)
+    rows.append(r)
+
+
+# ---------------------------------------------------------------------------------------------- a2
+def row_a2(rows, reps):
+    """lgx_build_norm_adj at C4 (500 M edges -> 1e9 nnz), plan excluded (dataloader.py:339-376)."""
+    cfg = CONFIGS["synth10m"]
+    u, i = synth_edges(cfg, 2020, DEV)
+    E, U, I = int(u.numel()), cfg.n_users, cfg.n_items
+    N = U + I
+    L = _lib.lib()
+    ws = ctypes.c_size_t(0)
+    _lib.check(L.lgx_build_norm_adj_workspace(E, U, I, ctypes.byref(ws)), "ws")
+    indptr = torch.empty(N + 1, dtype=torch.int64, device=DEV)
+    indices = torch.empty(2 * E, dtype=torch.int32, device=DEV)
+    vals = torch.empty(2 * E, dtype=torch.float32, device=DEV)
+    work = torch.empty(ws.value, dtype=torch.uint8, device=DEV)
+    st = torch.cuda.current_stream().cuda_stream
+
+    def run():
+        _lib.check(L.lgx_build_norm_adj(u.data_ptr(), i.data_ptr(), E, U, I, 1, indptr.data_ptr(),
+                                        indices.data_ptr(), vals.data_ptr(), work.data_ptr(), ws.value, st),
+                   "lgx_build_norm_adj")
+    ms = gpu_ms(run, max(1, reps // 2))
+    algo = E * 8 + 2 * E * 8 + (N + 1) * 8  # read the pairs, write indices + values, indptr
+    del indices, vals, work, indptr
+    # CPU: the oracle's restatement of the scipy build (C, one thread) on the ML-1M-shaped graph
+    c1 = CONFIGS["ml1m"]
+    cu, ci = synth_edges(c1, 2020, DEV)
+    cu, ci = cu.cpu().numpy(), ci.cpu().numpy()
+    s = cpu_s(lambda: oracle.build_norm_adj(cu, ci, c1.n_users, c1.n_items, dedup=True))
+    emit(rows, "a2 adjacency build (lgx_build_norm_adj)", ms, E, "edges/s", "hbm", algo, len(cu), s,
+         f"ML-1M-shaped graph ({len(cu)} edges), oracle C restatement", 1,
+         "radix sort of packed keys + 5 streaming passes; algorithmic = 8 B/edge in + 16 B/nnz out")
+    del u, i
+    torch.cuda.empty_cache()
+
+
+# ------------------------------------------------------------------------------------- a6 + a9
+def row_a6_a9(rows, reps):
+    """getUsersRating [B, I] (model.py:179-184) and the row top-K of tools.h:13-33 on it."""
+    B, I, d, k = 4096, 1_000_000, 256, 20
+    Q = ops.fill_normal((B, d), 1.0 / 16, 1, dtype=torch.bfloat16)
+    items = ops.fill_normal((I, d), 1.0 / 16, 2, dtype=torch.bfloat16)
+    S = ops.score_dense(Q, items)
+    ms = gpu_ms(lambda: ops.score_dense(Q, items), reps)
+    Qc, Ic = Q[:64].float().cpu(), items.float().cpu()
+    torch.set_num_threads(CPU_THREADS)
+    s = cpu_s(lambda: torch.sigmoid(torch.matmul(Qc, Ic.t())))
+    emit(rows, "a6 dense scoring (lgx_score_dense)", ms, B * I, "scores/s", "hbm", 4 * B * I + 2 * I * d + 2 * B * d,
+         64 * I, s, f"64 users x {I} items, d={d} fp32 torch.matmul + sigmoid", CPU_THREADS,
+         f"bf16 in, f32 out [B, I]; flops {2 * B * I * d:.3g} (MFMA well under its roof: write-bound)")
+    ms = gpu_ms(lambda: ops.topk_rows(S, k), reps)
+    Sc = S[:256].cpu()
+    s = cpu_s(lambda: torch.topk(Sc, k))
+    emit(rows, "a9 row top-K (lgx_topk_rows)", ms, B * I, "scores/s", "hbm", 4 * B * I + 8 * B * k,
+         256 * I, s, f"256 rows x {I} torch.topk(k={k})", CPU_THREADS)
+    del S, Q, items
+    torch.cuda.empty_cache()
+
+
+# ---------------------------------------------------------------------------------------------- a10
+def row_a10(rows, reps):
+    """evaluate_foldout (evaluate_foldout.h:115-195) for 1 M users, top-20, 10 truths each."""
+    users, k, T, I = 1_000_000, 20, 10, 1_000_000
+    g = torch.Generator(device=DEV).manual_seed(5)
+    rank = torch.randint(0, I, (users, k), device=DEV, dtype=torch.int32, generator=g)
+    tp = torch.arange(0, users * T + 1, T, device=DEV, dtype=torch.int64)
+    ti = torch.randint(0, I, (users * T,), device=DEV, dtype=torch.int32, generator=g)
+    ms = gpu_ms(lambda: ops.foldout_metrics(rank, (tp, ti)), reps)
+    n = 100_000
+    r_h = rank[:n].cpu().numpy()
+    t_h = ti[:n * T].cpu().numpy().reshape(n, T).tolist()
+    s = cpu_s(lambda: oracle.evaluate_foldout(r_h, t_h))
+    emit(rows, "a10 fold-out metrics (lgx_foldout_metrics)", ms, users, "users/s", "hbm",
+         users * (4 * k + 4 * T + 8 + 4 * 5 * k), n, s, f"{n} users, oracle C restatement", 1)
+
+
+# ---------------------------------------------------------------------------------------------- a12
+def row_a12(rows, reps):
+    """recommend.accuracy_cf (recommend.py:208-223): 1000 candidates per user, d=64 fp32, top-20."""
+    U, I, C, d, K = 100_000, 1_000_000, 1000, 64, 20
+    eu = ops.fill_normal((U, d), 0.1, 3)
+    ei = ops.fill_normal((I, d), 0.1, 4)
+    g = torch.Generator(device=DEV).manual_seed(6)
+    cand = torch.randint(0, I, (U * C,), device=DEV, dtype=torch.int32, generator=g)
+    cp = torch.arange(0, U * C + 1, C, device=DEV, dtype=torch.int64)
+
+    def run():
+        sc = ops.gather_scores(eu, ei, (cp, cand), U * C)
+        return ops.topk_rows(sc.view(U, C), K)
+    ms = gpu_ms(run, reps)
+    n = 2000
+    eu_h, ei_h = eu[:n].cpu().numpy(), ei.cpu().numpy()
+    c_h = cand[:n * C].cpu().numpy().reshape(n, C)
+
+    def cpu():  # the reference's per-user numpy dot + argpartition (recommend.py:214-217, :53-56)
+        for u in range(n):
+            s_ = np.dot(ei_h[c_h[u]], eu_h[u])
+            np.argpartition(s_, -K)[-K:]
+    s = cpu_s(cpu)
+    emit(rows, "a12 candidate scoring + top-K (lgx_gather_scores + lgx_topk_rows)", ms, U * C, "pairs/s", "hbm",
+         U * C * (4 + 4 * d + 4) + U * d * 4 + U * C * 4 + U * K * 8, n * C, s,
+         f"{n} users x {C} candidates, numpy dot + argpartition per user", 1,
+         "gathered item rows counted at 4*d B each (table 256 MB: L2/MALL serve part of them)")
+
+
+# ------------------------------------------------------------------------------------------ (f) 1
+def row_f1(rows, reps):
+    """recommend.difference max-dot of candidates vs train history (recommend.py:287-312)."""
+    U, I, C, H, d = 20_000, 1_000_000, 1000, 50, 64
+    ei = ops.fill_normal((I, d), 0.1, 7)
+    g = torch.Generator(device=DEV).manual_seed(8)
+    a = (torch.arange(0, U * C + 1, C, device=DEV, dtype=torch.int64),
+         torch.randint(0, I, (U * C,), device=DEV, dtype=torch.int32, generator=g))
+    b = (torch.arange(0, U * H + 1, H, device=DEV, dtype=torch.int64),
+         torch.randint(0, I, (U * H,), device=DEV, dtype=torch.int32, generator=g))
+    ms = gpu_ms(lambda: ops.list_dot_reduce(ei, a, b, "max"), reps)
+    n = 300
+    T = ei.cpu().numpy()
+    A = a[1][:n * C].cpu().numpy().reshape(n, C)
+    Bh = b[1][:n * H].cpu().numpy().reshape(n, H)
+
+    def cpu():  # recommend.py:305-307: numpy dot of the candidate and history rows, max per candidate
+        for u in range(n):
+            (T[A[u]] @ T[Bh[u]].T).max(axis=1)
+    s = cpu_s(cpu)
+    emit(rows, "f1 list x list max-dot (lgx_list_dot_reduce)", ms, U * C * H, "dots/s", "mfma_f32",
+         2.0 * U * C * H * d, n * C * H, s, f"{n} users x {C} x {H}, numpy f32 per user", 1,
+         "f32 tables: priced against the 157 TF f32 matrix peak")
+
+
+# ------------------------------------------------------------------------------------------ (f) 2
+def _np_sample(indptr, items, n_items, rng):
+    """Vectorised restatement of sampling.cpp:27-86 (one positive + one negative per train row,
+    negatives redrawn while they hit the user's positives)."""
+    n_users = len(indptr) - 1
+    deg = np.diff(indptr)
+    users = np.repeat(np.arange(n_users, dtype=np.int64), deg)
+    pos = items[indptr[users] + rng.integers(0, deg[users])]
+    keys = users * n_items + items.astype(np.int64)  # sorted: CSR rows ascending, items sorted
+    neg = rng.integers(0, n_items, len(users))
+    todo = np.arange(len(users))
+    while len(todo):
+        q = users[todo] * n_items + neg[todo]
+        j = np.minimum(np.searchsorted(keys, q), len(keys) - 1)
+        hit = keys[j] == q
+        todo = todo[hit]
+        neg[todo] = rng.integers(0, n_items, len(todo))
+    return users, pos, neg
+
+
+def row_f2(rows, reps):
+    """UniformSample_original through lgx_sample_bpr: one (user, pos, neg) row per train edge."""
+    U, I, P = 1_000_000, 1_000_000, 50
+    g = torch.Generator(device=DEV).manual_seed(9)
+    it = torch.randint(0, I, (U, P), device=DEV, dtype=torch.int32, generator=g)
+    it = torch.sort(it, dim=1).values.reshape(-1).contiguous()
+    ip = torch.arange(0, U * P + 1, P, device=DEV, dtype=torch.int64)
+    ms = gpu_ms(lambda: sampling.sample_device((ip, it), I, per_user=P, seed_value=1, drop_invalid=False), reps)
+    n = 200_000
+    ip_h, it_h = ip[:n + 1].cpu().numpy(), it[:n * P].cpu().numpy()
+    s = cpu_s(lambda: _np_sample(ip_h, it_h, I, np.random.default_rng(1)))
+    emit(rows, "f2 BPR sampler (lgx_sample_bpr)", ms, U * P, "samples/s", "hbm", U * P * (12 + 4 * 6) + U * 8, n * P, s,
+         f"{n} users x {P} rows, vectorised numpy restatement", 1,
+         "algorithmic: 12 B row out + ~6 probes of 4 B (positive draw + binary search) per row")
+
+
+# ------------------------------------------------------------------------------------------ (f) 3
+def row_f3(rows, reps, tmpdir):
+    """The uid item item ... train.txt parser (dataloader.py:247-277) on the device."""
+    rng = np.random.default_rng(10)
+    n_lines, per = 200_000, 50
+    its = rng.integers(0, 1_000_000, (n_lines, per))
+    lines = [str(u) + " " + " ".join(map(str, its[u])) for u in range(n_lines)]
+    data = ("\n".join(lines) + "\n").encode()
+    text = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(DEV)
+    ms = gpu_ms(lambda: ops.parse_lines(text), reps)
+    n = 20_000
+    path = os.path.join(tmpdir, "rows_train.txt")
+    with open(path, "wb") as f:
+        f.write(("\n".join(lines[:n]) + "\n").encode())
+    s = cpu_s(lambda: oracle.parse_lightgcn_txt(path, path))
+    emit(rows, "f3 interaction-file parse (lgx_parse_lines_count/fill)", ms, len(data), "bytes/s", "hbm",
+         len(data) + n_lines * per * 8 + n_lines * 12, len("\n".join(lines[:n]).encode()), s,
+         f"{n} lines, python line loop (oracle restatement of the Loader)", 1)
+
+
+# ------------------------------------------------------------------------------------------ (f) 4
+def row_f4(rows, reps):
+    """create_candidates_stratification labels + per-label picks (recommend.py:314-452), one
+    4096-user batch against 1 M items, d=64 fp32."""
+    B, I, d, F, Kc = 4096, 1_000_000, 64, 10, 1000
+    eu = ops.fill_normal((B, d), 0.1, 11)
+    ei = ops.fill_normal((I, d), 0.1, 12)
+    g = torch.Generator(device=DEV).manual_seed(13)
+    mi = torch.sort(torch.randint(0, I, (B, 50), device=DEV, dtype=torch.int32, generator=g), dim=1).values
+    mi = mi.reshape(-1).contiguous()
+    mp = torch.arange(0, B * 50 + 1, 50, device=DEV, dtype=torch.int64)
+    min16, inter16 = recommend.stratification_bounds(eu, ei, F, 0.1)
+    L = _lib.lib()
+    st = torch.cuda.current_stream().cuda_stream
+    S = ops.score_dense(eu, ei)
+    labels = torch.empty((B, I), dtype=torch.int8, device=DEV)
+    hist = torch.empty((B, F + 1), dtype=torch.int32, device=DEV)
+    tgt = torch.full((B,), Kc, dtype=torch.int32, device=DEV)
+    out = torch.empty((B, Kc), dtype=torch.int32, device=DEV)
+    cnt = torch.empty(B, dtype=torch.int32, device=DEV)
+
+    def lab():
+        _lib.check(L.lgx_strat_labels(S.data_ptr(), B, I, min16, inter16, F, mp.data_ptr(), mi.data_ptr(),
+                                      labels.data_ptr(), hist.data_ptr(), st), "lgx_strat_labels")
+
+    def sel():
+        _lib.check(L.lgx_strat_select(labels.data_ptr(), B, I, hist.data_ptr(), F + 1, tgt.data_ptr(), 77,
+                                      out.data_ptr(), Kc, cnt.data_ptr(), st), "lgx_strat_select")
+    ms_s = gpu_ms(lambda: ops.score_dense(eu, ei), reps)
+    ms_l = gpu_ms(lab, reps)
+    ms_p = gpu_ms(sel, reps)
+    n = 200
+    eu_h, ei_h = eu[:n].cpu().numpy(), ei.cpu().numpy()
+    tr = mi[:n * 50].cpu().numpy().reshape(n, 50).tolist()
+    s = cpu_s(lambda: oracle.stratification_labels(eu_h, ei_h, tr, F, 0.1))
+    emit(rows, "f4 stratified candidates: scores + labels + select (lgx_score_dense, lgx_strat_labels, "
+         "lgx_strat_select)", ms_s + ms_l + ms_p, B * I, "user-item pairs/s", "hbm", B * I * (4 + 4 + 1 + 1),
+         n * I, s, f"{n} users x {I} items: numpy dot + float16 labels + histograms (labels only)", 1,
+         f"per batch: score_dense {ms_s:.2f} ms, labels {ms_l:.2f} ms, select {ms_p:.2f} ms; algorithmic "
+         "10 B per pair (score write + read, label write + read)")
+    del S, labels
+    torch.cuda.empty_cache()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "rows.json"))
+    ap.add_argument("--only", default="")
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    if not torch.cuda.is_available():
+        raise SystemExit("bench_rows needs a GPU")
+    torch.set_num_threads(CPU_THREADS)
+    want = set(x for x in args.only.split(",") if x)
+    tmpdir = os.environ.get("TMPDIR", "/tmp")
+    steps = [("a2", lambda r: row_a2(r, args.reps)), ("a6", lambda r: row_a6_a9(r, args.reps)),
+             ("a10", lambda r: row_a10(r, args.reps)), ("a12", lambda r: row_a12(r, args.reps)),
+             ("f1", lambda r: row_f1(r, args.reps)), ("f2", lambda r: row_f2(r, args.reps)),
+             ("f3", lambda r: row_f3(r, args.reps, tmpdir)), ("f4", lambda r: row_f4(r, args.reps))]
+    rows = []
+    failed = []
+    for name, fn in steps:
+        if want and name not in want:
+            continue
+        try:
+            fn(rows)
+        except Exception as e:  # report and go on: one row's failure must not hide the others
+            print(json.dumps({"row": name, "error": repr(e)}), flush=True)
+            failed.append(name)
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    with open(args.out, "w") as f:
+        json.dump({"device": torch.cuda.get_device_name(0), "rows": rows, "failed": failed}, f, indent=1)
+    if failed:
+        raise SystemExit(f"rows failed: {failed}")
+
+
+if __name__ == "__main__":
+    main()
