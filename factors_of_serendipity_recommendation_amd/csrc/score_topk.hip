@@ -948,37 +948,59 @@ __global__ void minmax_init(uint32_t* mm) {
 // ---------------------------------------------------------------------------- dense scores
 // getUsersRating: users are the A operand (rows), items the B operand (lane columns) so that
 // each store instruction writes 32 consecutive floats of one user row.
+// A workgroup is 8 waves x 32 users = 256 users that walk the SAME 32-item tiles of one catalog
+// split in the same order, so a tile comes from HBM once per 256 users (the other waves find it in
+// L1/L2) instead of once per 32: at [4096, 1M] d=256 that is 8 GB of item reads next to the 16 GB of
+// scores written, not 64 GB.  Workgroup -> (user group, split) is XCD-aware: the workgroups of one
+// XCD (blockIdx mod 8) take splits s = xcd (mod 8), all user groups of a split back to back, so the
+// groups sharing a split also share that XCD's L2.
+constexpr int kDenseWaves = 8;
+constexpr int kDenseUsers = kDenseWaves * kUsersPerWave;
+
 template <int DT, int KCH>
-__global__ __launch_bounds__(256) void score_dense_kernel(const void* Q, const int64_t* user_rows, const void* items,
-                                                          int64_t B, int64_t n_items, int64_t d, int apply_sigmoid,
-                                                          float* __restrict__ out) {
+__global__ __launch_bounds__(kDenseWaves * 64) void score_dense_kernel(const void* Q, const int64_t* user_rows,
+                                                                        const void* items, int64_t B, int64_t n_items,
+                                                                        int64_t d, int apply_sigmoid,
+                                                                        float* __restrict__ out, int64_t n_ug,
+                                                                        int64_t split_items) {
     typedef Frag<DT> F;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, col = lane & 31;
-    const int64_t u0 = (int64_t)blockIdx.x * 32;
+    const int64_t L = blockIdx.x, kk = L >> 3;
+    const int64_t ug = kk % n_ug;
+    const int64_t split = (kk / n_ug) * 8 + (L & 7);
+    const int64_t u0 = ug * kDenseUsers + (int64_t)wave * kUsersPerWave;
+    if (u0 >= B) return;  // whole wave idle (no workgroup barrier in this kernel)
     const int64_t b = u0 + col;
     const bool user_ok = b < B;
     const int64_t qrow = user_ok ? (user_rows ? user_rows[b] : b) : 0;
     typename F::chunk uf[KCH];
 #pragma unroll
     for (int c = 0; c < KCH; ++c) uf[c] = F::load(Q, qrow, d, c, h, user_ok);
-    const int64_t tiles = (n_items + 31) / 32;
-    for (int64_t t = (int64_t)blockIdx.y * kWavesPerBlock + wave; t < tiles; t += (int64_t)gridDim.y * kWavesPerBlock) {
-        const int64_t i0 = t * 32;
+    const int64_t i_begin = split * split_items;
+    const int64_t i_end = std::min(n_items, i_begin + split_items);
+    // the next tile's item fragments are in flight while this tile's MFMAs and stores run
+    typename F::chunk fr[KCH];
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) fr[c] = F::load(items, i_begin + col, d, c, h, i_begin + col < i_end);
+    for (int64_t i0 = i_begin; i0 < i_end; i0 += 32) {
         const int64_t item_row = i0 + col;
-        const bool item_ok = item_row < n_items;
+        const bool item_ok = item_row < i_end;
         f32x16 acc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
 #pragma unroll
-        for (int c = 0; c < KCH; ++c) acc = F::mma(uf[c], F::load(items, item_row, d, c, h, item_ok), acc);
+        for (int c = 0; c < KCH; ++c) {
+            acc = F::mma(uf[c], fr[c], acc);
+            fr[c] = F::load(items, item_row + 32, d, c, h, item_row + 32 < i_end);
+        }
         if (!item_ok) continue;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int64_t u = u0 + tile_row(r, h);
             if (u < B) {
-                const float s = acc[r];
-                out[u * n_items + item_row] = apply_sigmoid ? 1.0f / (1.0f + expf(-s)) : s;
+                const float sc = acc[r];
+                out[u * n_items + item_row] = apply_sigmoid ? 1.0f / (1.0f + expf(-sc)) : sc;
             }
         }
     }
@@ -1276,12 +1298,17 @@ extern "C" int lgx_score_dense(const void* Q, const int64_t* user_rows, const vo
     LGX_REQUIRE(d > 0 && d % vec == 0 && kch > 0, LGX_ERR_UNSUPPORTED,
                 "lgx_score_dense: d=%lld must be a multiple of %lld and <= 256", (long long)d, (long long)vec);
     if (B == 0 || n_items == 0) return LGX_OK;
-    const int64_t ub = ceil_div(B, 32);
+    // splits: a multiple of 8 (one residue class per XCD), enough workgroups to fill the chip
+    const int64_t n_ug = ceil_div(B, (int64_t)kDenseUsers);
     const int64_t tiles = ceil_div(n_items, 32);
-    int64_t gy = std::max<int64_t>(1, std::min<int64_t>(ceil_div(2048, ub), ceil_div(tiles, kWavesPerBlock)));
-    dim3 grid((unsigned)ub, (unsigned)std::min<int64_t>(gy, 65535));
-#define LGX_SD(DTV, KC) score_dense_kernel<DTV, KC><<<grid, 256, 0, stream>>>(Q, user_rows, items, B, n_items, d, \
-                                                                              apply_sigmoid, scores)
+    const int64_t n_splits = std::max<int64_t>(8, std::min(8 * ceil_div(ceil_div(2048, n_ug), 8), 8 * ceil_div(tiles, 8)));
+    const int64_t split_items = 32 * ceil_div(tiles, n_splits);
+    const int64_t grid = n_ug * n_splits;
+    LGX_REQUIRE(grid < (1LL << 31), LGX_ERR_UNSUPPORTED, "lgx_score_dense: %lld users is too many", (long long)B);
+#define LGX_SD(DTV, KC)                                                                                \
+    score_dense_kernel<DTV, KC><<<(unsigned)grid, kDenseWaves * 64, 0, stream>>>(Q, user_rows, items, B, n_items, \
+                                                                                 d, apply_sigmoid, scores, n_ug,  \
+                                                                                 split_items)
 #define LGX_SD_ALL(DTV)                  \
     switch (kch) {                       \
         case 2: LGX_SD(DTV, 2); break;   \

@@ -28,18 +28,22 @@ namespace {
 constexpr int kStratThreads = 256;
 constexpr int kMaxFolds = 32;
 constexpr int kMaxStratK = 1024;  // candidates per user that the selection kernel keeps in LDS
+constexpr int kMaxCand = 2048;    // fast-path candidates (13 B each) in the radix histogram's 32 KB
 
 __device__ __forceinline__ float half_round(float x) { return __half2float(__float2half_rn(x)); }
 
-__device__ __forceinline__ bool in_sorted_list(const int32_t* __restrict__ a, int64_t begin, int64_t end, int32_t v) {
-    int64_t lo = begin, hi = end;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (a[mid] < v) lo = mid + 1; else hi = mid;
-    }
-    return lo < end && a[lo] == v;
+__device__ __forceinline__ int label_of(float sc, float min16, float inter16, int num_fold) {
+    // numpy float16: every operation in float, rounded back to half
+    const float d = half_round(half_round(sc) - min16);
+    const float q = half_round(d / inter16);
+    const int lv = (int)floorf(q);
+    return lv < 0 ? 0 : (lv > num_fold ? num_fold : lv);  // d >= 0; the top bin is label num_fold
 }
 
+// Labels of every item first (4 per thread and float4 / 32-bit accesses when rows are 16-B
+// aligned), then the user's train items are relabelled -1 and taken out of the histogram: one
+// pass over the row instead of a binary search of the mask per item.
+template <bool VEC4>
 __global__ __launch_bounds__(kStratThreads) void strat_labels_kernel(const float* __restrict__ scores, int64_t n_items,
                                                                     float min16, float inter16, int num_fold,
                                                                     const int64_t* __restrict__ mask_indptr,
@@ -50,20 +54,37 @@ __global__ __launch_bounds__(kStratThreads) void strat_labels_kernel(const float
     const int64_t u = blockIdx.x;
     if (threadIdx.x < kMaxFolds) h[threadIdx.x] = 0;
     __syncthreads();
-    const int64_t m0 = mask_indptr ? mask_indptr[u] : 0, m1 = mask_indptr ? mask_indptr[u + 1] : 0;
     const float* s = scores + u * n_items;
     int8_t* lab = labels + u * n_items;
-    for (int64_t i = threadIdx.x; i < n_items; i += kStratThreads) {
-        int lv = -1;
-        if (!in_sorted_list(mask_indices, m0, m1, (int32_t)i)) {
-            // numpy float16: every operation in float, rounded back to half
-            const float d = half_round(half_round(s[i]) - min16);
-            const float q = half_round(d / inter16);
-            lv = (int)floorf(q);
-            lv = lv < 0 ? 0 : (lv > num_fold ? num_fold : lv);  // d >= 0; the top bin is label num_fold
-            atomicAdd(&h[lv], 1);
+    if (VEC4) {
+        const int64_t n4 = n_items >> 2;
+        for (int64_t q = threadIdx.x; q < n4; q += kStratThreads) {
+            const float4 v = reinterpret_cast<const float4*>(s)[q];
+            const int l0 = label_of(v.x, min16, inter16, num_fold), l1 = label_of(v.y, min16, inter16, num_fold);
+            const int l2 = label_of(v.z, min16, inter16, num_fold), l3 = label_of(v.w, min16, inter16, num_fold);
+            atomicAdd(&h[l0], 1);
+            atomicAdd(&h[l1], 1);
+            atomicAdd(&h[l2], 1);
+            atomicAdd(&h[l3], 1);
+            reinterpret_cast<uint32_t*>(lab)[q] = (uint32_t)l0 | ((uint32_t)l1 << 8) | ((uint32_t)l2 << 16) |
+                                                  ((uint32_t)l3 << 24);
         }
-        lab[i] = (int8_t)lv;
+    } else {
+        for (int64_t i = threadIdx.x; i < n_items; i += kStratThreads) {
+            const int lv = label_of(s[i], min16, inter16, num_fold);
+            atomicAdd(&h[lv], 1);
+            lab[i] = (int8_t)lv;
+        }
+    }
+    __syncthreads();  // the row's labels (global) and counts are complete before the mask fix-up
+    if (mask_indptr) {
+        const int64_t m0 = mask_indptr[u], m1 = mask_indptr[u + 1];
+        for (int64_t j = m0 + threadIdx.x; j < m1; j += kStratThreads) {
+            const int32_t it = mask_indices[j];
+            if (it < 0 || it >= n_items || (j > m0 && mask_indices[j - 1] == it)) continue;  // sorted: skip repeats
+            atomicSub(&h[label_of(s[it], min16, inter16, num_fold)], 1);
+            lab[it] = -1;
+        }
     }
     __syncthreads();
     if (threadIdx.x <= num_fold) hist[u * (num_fold + 1) + threadIdx.x] = h[threadIdx.x];
@@ -81,7 +102,12 @@ __global__ __launch_bounds__(kStratThreads) void strat_select_kernel(const int8_
                                                                     const int32_t* __restrict__ targets, uint64_t seed,
                                                                     int32_t* __restrict__ out, int out_stride,
                                                                     int32_t* __restrict__ out_count) {
-    __shared__ uint32_t dh[kMaxFolds * 256];  // per (label, 8-bit digit) counts
+    // per (label, 8-bit digit) counts of the exact radix path; the fast path keeps its candidates
+    // (keys, items, labels) in the same bytes
+    __shared__ __attribute__((aligned(16))) uint32_t dh[kMaxFolds * 256];
+    __shared__ int32_t n_cand, cand_l[kMaxFolds];
+    __shared__ uint64_t cut[kMaxFolds];
+    __shared__ int fast_ok;
     __shared__ int64_t need[kMaxFolds];       // keys still to take below the threshold being refined
     __shared__ uint64_t prefix[kMaxFolds];    // threshold bits fixed so far
     __shared__ uint64_t keys_sh[kMaxStratK];
@@ -103,9 +129,64 @@ __global__ __launch_bounds__(kStratThreads) void strat_select_kernel(const int8_
         n_sel = 0;
     }
     __syncthreads();
+    // Fast path: the keys are uniform 64-bit hashes, so the need[l] smallest of label l lie below
+    // cut[l] = 2^64 (need[l] + 4 sqrt(need[l]) + 8) / hist[l] but for a ~4-sigma shortfall.  One pass
+    // gathers every key under its label's cut into LDS (expected K + a few hundred), and the exact
+    // need[l] smallest per label are ranked there: the same picks as the radix select below, which
+    // runs only when a label came up short or the buffer overflowed.
+    uint64_t* ck = reinterpret_cast<uint64_t*>(dh);
+    int32_t* ci = reinterpret_cast<int32_t*>(ck + kMaxCand);
+    int8_t* cl = reinterpret_cast<int8_t*>(ci + kMaxCand);
+    if (tid < n_bins) {
+        const int64_t hl = hist[u * n_bins + tid], nl = need[tid];
+        const double frac = hl > 0 ? ((double)nl + 4.0 * sqrt((double)nl) + 8.0) / (double)hl : 2.0;
+        cut[tid] = nl <= 0 ? 0ull : (frac >= 1.0 ? ~0ull : (uint64_t)(frac * 18446744073709551616.0));
+        cand_l[tid] = 0;
+    }
+    if (tid == 0) n_cand = 0;
+    __syncthreads();
+    for (int64_t i = tid; i < n_items; i += kStratThreads) {
+        const int l = lab[i];
+        if (l < 0 || l >= n_bins || need[l] <= 0) continue;
+        const uint64_t k = item_key(seed, u, i);
+        if (k > cut[l]) continue;
+        atomicAdd(&cand_l[l], 1);
+        const int slot = atomicAdd(&n_cand, 1);
+        if (slot < kMaxCand) {
+            ck[slot] = k;
+            ci[slot] = (int32_t)i;
+            cl[slot] = (int8_t)l;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int ok = n_cand <= kMaxCand;
+        for (int l = 0; l < n_bins; ++l) ok &= need[l] <= 0 || cand_l[l] >= need[l];
+        fast_ok = ok;
+    }
+    __syncthreads();
+    if (fast_ok) {
+        // rank of each candidate inside its label by (key, item); the need[l] lowest are taken
+        const int m = n_cand;
+        for (int a = tid; a < m; a += kStratThreads) {
+            const uint64_t ka = ck[a];
+            const int la = cl[a], ia = ci[a];
+            int r = 0;
+            for (int b2 = 0; b2 < m; ++b2)
+                r += (cl[b2] == la && (ck[b2] < ka || (ck[b2] == ka && ci[b2] < ia))) ? 1 : 0;
+            if (r < need[la]) {
+                const int slot = atomicAdd(&n_sel, 1);
+                if (slot < kMaxStratK) {
+                    keys_sh[slot] = ka;
+                    items_sh[slot] = ia;
+                }
+            }
+        }
+        __syncthreads();
+    }
     // radix select, 8 passes of 8 bits from the top: after pass p, prefix[l] holds the top 8(p+1)
     // bits of the need[l]-th smallest key of label l (need[l] counts down the keys already below it)
-    for (int pass = 0; pass < 8; ++pass) {
+    for (int pass = 0; pass < 8 && !fast_ok; ++pass) {
         const int shift = 56 - 8 * pass;
         for (int j = tid; j < n_bins * 256; j += kStratThreads) dh[j] = 0;
         __syncthreads();
@@ -136,7 +217,7 @@ __global__ __launch_bounds__(kStratThreads) void strat_select_kernel(const int8_
     }
     // take every key below the label's threshold, plus need[l] keys equal to it (ties: a 64-bit
     // hash collision; taken in arrival order)
-    for (int64_t i = tid; i < n_items; i += kStratThreads) {
+    for (int64_t i = tid; i < n_items && !fast_ok; i += kStratThreads) {
         const int l = lab[i];
         if (l < 0 || l >= n_bins) continue;
         const uint64_t k = item_key(seed, u, i);
@@ -188,8 +269,13 @@ extern "C" int lgx_strat_labels(const float* scores, int64_t n_users, int64_t n_
     if (n_users == 0) return LGX_OK;
     LGX_REQUIRE(scores && labels && hist && (!mask_indptr || mask_indices), LGX_ERR_INVALID_ARG,
                 "lgx_strat_labels: null pointer");
-    strat_labels_kernel<<<(unsigned)n_users, kStratThreads, 0, as_hip(stream)>>>(
-        scores, n_items, min16, inter16, num_fold, mask_indptr, mask_indices, labels, hist);
+    const bool vec4 = n_items % 4 == 0 && ((uintptr_t)scores & 15) == 0 && ((uintptr_t)labels & 3) == 0;
+    if (vec4)
+        strat_labels_kernel<true><<<(unsigned)n_users, kStratThreads, 0, as_hip(stream)>>>(
+            scores, n_items, min16, inter16, num_fold, mask_indptr, mask_indices, labels, hist);
+    else
+        strat_labels_kernel<false><<<(unsigned)n_users, kStratThreads, 0, as_hip(stream)>>>(
+            scores, n_items, min16, inter16, num_fold, mask_indptr, mask_indices, labels, hist);
     LGX_LAUNCH_CHECK();
     return LGX_OK;
 }
