@@ -48,6 +48,57 @@ __global__ __launch_bounds__(256) void gather_scores_kernel(const float* __restr
     if (gl == 0) out[p] = s;
 }
 
+// The same dots walked user by user: one wave per user, 64/G groups of G lanes each take every
+// (64/G)-th candidate, the user's row stays in registers and U item rows are in flight per group.
+// No per-pair search for the owning user; per lane the same fmaf order and the same xor-shuffle
+// reduction as gather_scores_kernel, so the scores are bit-identical.
+template <int G, int CH, int U>
+__global__ __launch_bounds__(256) void gather_scores_by_user(const float* __restrict__ eu, const float* __restrict__ ei,
+                                                             int64_t n_users, int64_t d,
+                                                             const int64_t* __restrict__ cand_indptr,
+                                                             const int32_t* __restrict__ cand_items,
+                                                             float* __restrict__ out) {
+    constexpr int GPW = 64 / G;
+    const int lane = threadIdx.x & 63, gl = lane & (G - 1), grp = lane / G;
+    const int64_t u = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    if (u >= n_users) return;
+    const int64_t p0 = cand_indptr[u], p1 = cand_indptr[u + 1];
+    float4 x[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+        const int64_t off = (int64_t)(gl + c * G) * 4;
+        x[c] = off < d ? *reinterpret_cast<const float4*>(eu + u * d + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    for (int64_t pb = p0 + grp; pb < p1; pb += (int64_t)GPW * U) {
+        float4 y[U][CH];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int64_t q = pb + (int64_t)j * GPW;
+            const float* b = ei + (q < p1 ? (int64_t)cand_items[q] : 0) * d;
+#pragma unroll
+            for (int c = 0; c < CH; ++c) {
+                const int64_t off = (int64_t)(gl + c * G) * 4;
+                y[j][c] = (q < p1 && off < d) ? *reinterpret_cast<const float4*>(b + off)
+                                              : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int64_t q = pb + (int64_t)j * GPW;
+            float s = 0.0f;
+#pragma unroll
+            for (int c = 0; c < CH; ++c) {
+                if ((int64_t)(gl + c * G) * 4 >= d) break;
+                s = fmaf(x[c].x, y[j][c].x, s); s = fmaf(x[c].y, y[j][c].y, s);
+                s = fmaf(x[c].z, y[j][c].z, s); s = fmaf(x[c].w, y[j][c].w, s);
+            }
+#pragma unroll
+            for (int m = G >> 1; m > 0; m >>= 1) s += __shfl_xor(s, m, G);
+            if (gl == 0 && q < p1) out[q] = s;
+        }
+    }
+}
+
 __global__ void synth_edges_kernel(uint64_t seed, const int64_t* __restrict__ offsets, int64_t n_users,
                                    const float* __restrict__ cdf, const int32_t* __restrict__ perm,
                                    int64_t n_items, int64_t n_edges, int32_t* __restrict__ users_out,
@@ -112,6 +163,21 @@ extern "C" int lgx_gather_scores(const float* emb_user, const float* emb_item, i
     LGX_REQUIRE(d > 0 && d % 4 == 0, LGX_ERR_UNSUPPORTED, "lgx_gather_scores: d must be a multiple of 4");
     if (n_pairs == 0) return LGX_OK;
     const int64_t chunks = d / 4;
+    if (chunks <= 64 * 4) {  // by user: one wave per user
+        const unsigned grid = (unsigned)ceil_div(n_users * 64, 256);
+#define LGX_GU(GV, CHV, UV) \
+    gather_scores_by_user<GV, CHV, UV><<<grid, 256, 0, stream>>>(emb_user, emb_item, n_users, d, cand_indptr, cand_items, scores)
+        if (chunks <= 4) LGX_GU(4, 1, 4);
+        else if (chunks <= 8) LGX_GU(8, 1, 4);
+        else if (chunks <= 16) LGX_GU(16, 1, 4);
+        else if (chunks <= 32) LGX_GU(32, 1, 4);
+        else if (chunks <= 64) LGX_GU(64, 1, 4);
+        else if (chunks <= 128) LGX_GU(64, 2, 2);
+        else LGX_GU(64, 4, 1);
+#undef LGX_GU
+        LGX_LAUNCH_CHECK();
+        return LGX_OK;
+    }
 #define LGX_GS(GV)                                                                                      \
     gather_scores_kernel<GV><<<ceil_div(n_pairs * GV, 256), 256, 0, stream>>>(emb_user, emb_item, n_users, \
                                                                               d, cand_indptr, cand_items, \

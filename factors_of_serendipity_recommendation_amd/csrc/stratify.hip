@@ -57,17 +57,29 @@ __global__ __launch_bounds__(kStratThreads) void strat_labels_kernel(const float
     const float* s = scores + u * n_items;
     int8_t* lab = labels + u * n_items;
     if (VEC4) {
+        // 4 float4 loads in flight per thread per iteration
+        constexpr int kU = 4;
         const int64_t n4 = n_items >> 2;
-        for (int64_t q = threadIdx.x; q < n4; q += kStratThreads) {
-            const float4 v = reinterpret_cast<const float4*>(s)[q];
-            const int l0 = label_of(v.x, min16, inter16, num_fold), l1 = label_of(v.y, min16, inter16, num_fold);
-            const int l2 = label_of(v.z, min16, inter16, num_fold), l3 = label_of(v.w, min16, inter16, num_fold);
-            atomicAdd(&h[l0], 1);
-            atomicAdd(&h[l1], 1);
-            atomicAdd(&h[l2], 1);
-            atomicAdd(&h[l3], 1);
-            reinterpret_cast<uint32_t*>(lab)[q] = (uint32_t)l0 | ((uint32_t)l1 << 8) | ((uint32_t)l2 << 16) |
-                                                  ((uint32_t)l3 << 24);
+        for (int64_t q0 = threadIdx.x; q0 < n4; q0 += kU * kStratThreads) {
+            float4 v[kU];
+#pragma unroll
+            for (int j = 0; j < kU; ++j) {
+                const int64_t q = q0 + j * kStratThreads;
+                v[j] = q < n4 ? reinterpret_cast<const float4*>(s)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int j = 0; j < kU; ++j) {
+                const int64_t q = q0 + j * kStratThreads;
+                if (q >= n4) break;
+                const int l0 = label_of(v[j].x, min16, inter16, num_fold), l1 = label_of(v[j].y, min16, inter16, num_fold);
+                const int l2 = label_of(v[j].z, min16, inter16, num_fold), l3 = label_of(v[j].w, min16, inter16, num_fold);
+                atomicAdd(&h[l0], 1);
+                atomicAdd(&h[l1], 1);
+                atomicAdd(&h[l2], 1);
+                atomicAdd(&h[l3], 1);
+                reinterpret_cast<uint32_t*>(lab)[q] = (uint32_t)(l0 & 255) | ((uint32_t)(l1 & 255) << 8) |
+                                                      ((uint32_t)(l2 & 255) << 16) | ((uint32_t)(l3 & 255) << 24);
+            }
         }
     } else {
         for (int64_t i = threadIdx.x; i < n_items; i += kStratThreads) {
@@ -97,6 +109,7 @@ __device__ __forceinline__ uint64_t item_key(uint64_t seed, int64_t u, int64_t i
 // np.rint: round half to even
 __device__ __forceinline__ int64_t rint_even(double x) { return (int64_t)rint(x); }
 
+template <bool VEC16>
 __global__ __launch_bounds__(kStratThreads) void strat_select_kernel(const int8_t* __restrict__ labels, int64_t n_items,
                                                                     const int32_t* __restrict__ hist, int n_bins,
                                                                     const int32_t* __restrict__ targets, uint64_t seed,
@@ -145,11 +158,10 @@ __global__ __launch_bounds__(kStratThreads) void strat_select_kernel(const int8_
     }
     if (tid == 0) n_cand = 0;
     __syncthreads();
-    for (int64_t i = tid; i < n_items; i += kStratThreads) {
-        const int l = lab[i];
-        if (l < 0 || l >= n_bins || need[l] <= 0) continue;
+    auto consider = [&](int64_t i, int l) {
+        if (l < 0 || l >= n_bins || need[l] <= 0) return;
         const uint64_t k = item_key(seed, u, i);
-        if (k > cut[l]) continue;
+        if (k > cut[l]) return;
         atomicAdd(&cand_l[l], 1);
         const int slot = atomicAdd(&n_cand, 1);
         if (slot < kMaxCand) {
@@ -157,6 +169,17 @@ __global__ __launch_bounds__(kStratThreads) void strat_select_kernel(const int8_
             ci[slot] = (int32_t)i;
             cl[slot] = (int8_t)l;
         }
+    };
+    if (VEC16) {  // 16 labels per 16-B load
+        const int64_t n16 = n_items >> 4;
+        for (int64_t q = tid; q < n16; q += kStratThreads) {
+            const uint4 w = reinterpret_cast<const uint4*>(lab)[q];
+            const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int j = 0; j < 16; ++j) consider(16 * q + j, (int)(int8_t)(ws[j >> 2] >> (8 * (j & 3))));
+        }
+    } else {
+        for (int64_t i = tid; i < n_items; i += kStratThreads) consider(i, lab[i]);
     }
     __syncthreads();
     if (tid == 0) {
@@ -289,8 +312,13 @@ extern "C" int lgx_strat_select(const int8_t* labels, int64_t n_users, int64_t n
                 "lgx_strat_select: at most %d candidates per user", kMaxStratK);
     if (n_users == 0) return LGX_OK;
     LGX_REQUIRE(labels && hist && targets && out && out_count, LGX_ERR_INVALID_ARG, "lgx_strat_select: null pointer");
-    strat_select_kernel<<<(unsigned)n_users, kStratThreads, 0, as_hip(stream)>>>(
-        labels, n_items, hist, n_bins, targets, seed, out, out_stride, out_count);
+    const bool vec16 = n_items % 16 == 0 && ((uintptr_t)labels & 15) == 0;
+    if (vec16)
+        strat_select_kernel<true><<<(unsigned)n_users, kStratThreads, 0, as_hip(stream)>>>(
+            labels, n_items, hist, n_bins, targets, seed, out, out_stride, out_count);
+    else
+        strat_select_kernel<false><<<(unsigned)n_users, kStratThreads, 0, as_hip(stream)>>>(
+            labels, n_items, hist, n_bins, targets, seed, out, out_stride, out_count);
     LGX_LAUNCH_CHECK();
     return LGX_OK;
 }

@@ -4,45 +4,76 @@
 // 13-33: std::partial_sort_copy per row on a host thread pool) and evaluate_foldout
 // (evaluator/cpp/include/evaluate_foldout.h:16-195).
 //
-// One 256-thread workgroup per row: each of its 4 waves streams an interleaved quarter of the
-// row with coalesced 256-B loads, filters against its running k-th key and merges survivors with
-// the register bitonic network of wave_topk.h; wave 0 then merges the other three lists.
+// Long rows: one 256-thread workgroup per row, each of its 4 waves streams an interleaved quarter
+// of the row with coalesced 1-KB (float4) loads, filters against its running k-th key and merges
+// survivors with the register bitonic network of wave_topk.h; the row's first wave then merges the
+// other three lists.  Short rows (< 16 K columns): one wave per row, 4 rows per workgroup.
 #include "wave_topk.h"
 
 namespace lgx {
 namespace {
 
-constexpr int kWavesPerRow = 4;
-constexpr int kUnroll = 4;
+constexpr int kUnroll = 2;
 
-__global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict__ S, int64_t cols,
+// WPR waves per row (4 for long rows, 1 for short ones: 4 rows per workgroup).  VEC: rows are
+// 16-B aligned, so each lane loads float4s (1 KB per wave instruction).  Per batch of loads one
+// integer compare of ord(score) against the running k-th key's score bits rules out the batch
+// (exact: ties and NaNs go to the merge, which orders by the full key).
+template <int WPR, bool VEC>
+__global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict__ S, int64_t rows, int64_t cols,
                                                         int64_t ld, int k, int32_t* __restrict__ out_idx,
                                                         float* __restrict__ out_val) {
-    __shared__ uint64_t lists[kWavesPerRow][kWave];
+    __shared__ uint64_t lists[4][kWave];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t row = blockIdx.x;
+    const int sub = wave % WPR;                       // this wave's part of its row
+    const int64_t row = (int64_t)blockIdx.x * (4 / WPR) + wave / WPR;
+    if (row >= rows) return;                          // no barrier is reached by a missing row's waves
     const float* s = S + row * ld;
     uint64_t top = 0;
-    const int64_t stride = (int64_t)kWave * kWavesPerRow;
-    for (int64_t base = (int64_t)wave * kWave; base < cols; base += stride * kUnroll) {
-        uint64_t cand[kUnroll];
+    constexpr int V = VEC ? 4 : 1;
+    const int64_t stride = (int64_t)kWave * V * WPR;  // columns per wave round
+    for (int64_t base = (int64_t)sub * kWave * V; base < cols; base += stride * kUnroll) {
+        float v[kUnroll][V];
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
-            const int64_t c = base + u * stride + lane;
-            cand[u] = c < cols ? make_key(s[c], (int32_t)c) : 0ull;
-        }
+            const int64_t c0 = base + u * stride + (int64_t)lane * V;
+            if (VEC) {
+                if (c0 + 3 < cols) {
+                    const float4 q = *reinterpret_cast<const float4*>(s + c0);
+                    v[u][0] = q.x; v[u][V > 1 ? 1 : 0] = q.y; v[u][V > 2 ? 2 : 0] = q.z; v[u][V > 3 ? 3 : 0] = q.w;
+                } else {
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) wave_topk_push(top, cand[u], k, lane);
+                    for (int j = 0; j < V; ++j) v[u][j] = c0 + j < cols ? s[c0 + j] : 0.0f;
+                }
+            } else {
+                v[u][0] = c0 < cols ? s[c0] : 0.0f;
+            }
+        }
+        const uint32_t thr_hi = (uint32_t)(shfl_u64(top, k - 1) >> 32);
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u)
+#pragma unroll
+            for (int j = 0; j < V; ++j) any |= base + u * stride + (int64_t)lane * V + j < cols && ord_f32(v[u][j]) >= thr_hi;
+        if (__ballot(any) == 0ull) continue;
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u)
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const int64_t c = base + u * stride + (int64_t)lane * V + j;
+                wave_topk_push(top, c < cols ? make_key(v[u][j], (int32_t)c) : 0ull, k, lane);
+            }
     }
-    lists[wave][lane] = top;
-    __syncthreads();
-    if (wave == 0) {
+    if (WPR > 1) {
+        lists[wave][lane] = top;
+        __syncthreads();
+        if (sub != 0) return;
 #pragma unroll
-        for (int w = 1; w < kWavesPerRow; ++w) wave_topk_push(top, lists[w][lane], k, lane);
-        if (lane < k) {
-            out_idx[row * k + lane] = top ? key_index(top) : -1;
-            if (out_val) out_val[row * k + lane] = top ? key_score(top) : -INFINITY;
-        }
+        for (int w = 1; w < WPR; ++w) wave_topk_push(top, lists[wave + w][lane], k, lane);
+    }
+    if (lane < k) {
+        out_idx[row * k + lane] = top ? key_index(top) : -1;
+        if (out_val) out_val[row * k + lane] = top ? key_score(top) : -INFINITY;
     }
 }
 
@@ -100,7 +131,16 @@ extern "C" int lgx_topk_rows(const float* S, int64_t rows, int64_t cols, int64_t
                 "lgx_topk_rows: bad arguments");
     LGX_REQUIRE(k >= 1 && k <= 64, LGX_ERR_UNSUPPORTED, "lgx_topk_rows: k=%d outside [1, 64]", k);
     if (rows == 0) return LGX_OK;
-    topk_rows_kernel<<<rows, 256, 0, as_hip(stream)>>>(S, cols, ld, k, out_idx, out_val);
+    const bool vec = ld % 4 == 0 && ((uintptr_t)S & 15) == 0;
+    hipStream_t st = as_hip(stream);
+    if (cols >= 16384) {
+        if (vec) topk_rows_kernel<4, true><<<(unsigned)rows, 256, 0, st>>>(S, rows, cols, ld, k, out_idx, out_val);
+        else topk_rows_kernel<4, false><<<(unsigned)rows, 256, 0, st>>>(S, rows, cols, ld, k, out_idx, out_val);
+    } else {
+        const unsigned grid = (unsigned)ceil_div(rows, 4);
+        if (vec) topk_rows_kernel<1, true><<<grid, 256, 0, st>>>(S, rows, cols, ld, k, out_idx, out_val);
+        else topk_rows_kernel<1, false><<<grid, 256, 0, st>>>(S, rows, cols, ld, k, out_idx, out_val);
+    }
     LGX_LAUNCH_CHECK();
     return LGX_OK;
 }
