@@ -1006,6 +1006,98 @@ __global__ __launch_bounds__(kDenseWaves * 64) void score_dense_kernel(const voi
     }
 }
 
+// The same walk with the item tile staged in LDS once per workgroup (KCH >= 8): one 16-B global
+// load per slot for the whole workgroup instead of one per wave, fragments read back with
+// ds_read_b128 from an XOR-swizzled image (slot ^ (row & 15): the 16 rows a lane group reads sit in
+// 16 different 4-bank groups).  Double-buffered: the next tile's loads are in flight during this
+// tile's MFMAs and stores; one barrier per tile, so idle waves (past B) still take part.
+template <int DT, int KCH>
+__global__ __launch_bounds__(kDenseWaves * 64) void score_dense_lds(const void* Q, const int64_t* user_rows,
+                                                                     const void* items, int64_t B, int64_t n_items,
+                                                                     int64_t d, int apply_sigmoid,
+                                                                     float* __restrict__ out, int64_t n_ug,
+                                                                     int64_t split_items) {
+    static_assert(KCH >= 8, "swizzle needs >= 16 slots per row");
+    typedef Frag<DT> F;
+    constexpr int SPR = 2 * KCH;           // 16-B slots per item row (a chunk = 32 B = two halves)
+    constexpr int RB = SPR * 16;           // row bytes of the image
+    constexpr int TILE = 32 * RB;
+    constexpr int NL = 32 * SPR / (kDenseWaves * 64);  // slots per thread per tile
+    static_assert(NL >= 1 && 32 * SPR % (kDenseWaves * 64) == 0, "tile slots must divide over the workgroup");
+    __shared__ __attribute__((aligned(16))) unsigned char img[2][TILE];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int h = lane >> 5, col = lane & 31;
+    const int64_t L = blockIdx.x, kk = L >> 3;
+    const int64_t ug = kk % n_ug;
+    const int64_t split = (kk / n_ug) * 8 + (L & 7);
+    const int64_t u0 = ug * kDenseUsers + (int64_t)wave * kUsersPerWave;
+    const bool wave_on = u0 < B;
+    const int64_t b = u0 + col;
+    const bool user_ok = b < B;
+    const int64_t qrow = user_ok ? (user_rows ? user_rows[b] : b) : 0;
+    typename F::chunk uf[KCH];
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) uf[c] = F::load(Q, qrow, d, c, h, user_ok);
+    const int64_t i_begin = split * split_items;
+    const int64_t i_end = std::min(n_items, i_begin + split_items);
+    const int64_t row_bytes = d * (DT == LGX_DTYPE_F32 ? 4 : 2);
+    const unsigned char* ib = static_cast<const unsigned char*>(items);
+    uint4 nx[NL];
+    auto load_tile = [&](int64_t i0) {
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int sl = threadIdx.x + j * kDenseWaves * 64;
+            const int r = sl / SPR, q = sl % SPR;
+            const int64_t it = i0 + r;
+            nx[j] = (it < i_end && q * 16 < row_bytes)
+                        ? *reinterpret_cast<const uint4*>(ib + it * row_bytes + q * 16)
+                        : make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
+    auto store_tile = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int sl = threadIdx.x + j * kDenseWaves * 64;
+            const int r = sl / SPR, q = sl % SPR;
+            *reinterpret_cast<uint4*>(&img[buf][r * RB + ((q ^ (r & 15)) * 16)]) = nx[j];
+        }
+    };
+    if (i_begin >= i_end) return;  // workgroup-uniform
+    load_tile(i_begin);
+    store_tile(0);
+    __syncthreads();
+    int buf = 0;
+    for (int64_t i0 = i_begin; i0 < i_end; i0 += 32) {
+        const bool more = i0 + 32 < i_end;  // workgroup-uniform
+        if (more) load_tile(i0 + 32);
+        if (wave_on) {
+            const unsigned char* rowp = &img[buf][col * RB];
+            f32x16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+            for (int c = 0; c < KCH; ++c) {
+                const uint4 fr = *reinterpret_cast<const uint4*>(rowp + (((2 * c + h) ^ (col & 15)) * 16));
+                acc = F::mma(uf[c], __builtin_bit_cast(typename F::chunk, fr), acc);
+            }
+            const int64_t item_row = i0 + col;
+            if (item_row < i_end) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t u = u0 + tile_row(r, h);
+                    if (u < B) {
+                        const float sc = acc[r];
+                        out[u * n_items + item_row] = apply_sigmoid ? 1.0f / (1.0f + expf(-sc)) : sc;
+                    }
+                }
+            }
+        }
+        if (more) store_tile(buf ^ 1);  // last read in the previous iteration, before its barrier
+        __syncthreads();
+        buf ^= 1;
+    }
+}
+
 int kch_for(int dtype, int64_t d) {
     const int64_t per = dtype == LGX_DTYPE_F32 ? 8 : 16;
     const int64_t c = (d + per - 1) / per;
@@ -1305,10 +1397,15 @@ extern "C" int lgx_score_dense(const void* Q, const int64_t* user_rows, const vo
     const int64_t split_items = 32 * ceil_div(tiles, n_splits);
     const int64_t grid = n_ug * n_splits;
     LGX_REQUIRE(grid < (1LL << 31), LGX_ERR_UNSUPPORTED, "lgx_score_dense: %lld users is too many", (long long)B);
-#define LGX_SD(DTV, KC)                                                                                \
-    score_dense_kernel<DTV, KC><<<(unsigned)grid, kDenseWaves * 64, 0, stream>>>(Q, user_rows, items, B, n_items, \
-                                                                                 d, apply_sigmoid, scores, n_ug,  \
-                                                                                 split_items)
+#define LGX_SD(DTV, KC)                                                                                    \
+    if constexpr (KC >= 8)                                                                                 \
+        score_dense_lds<DTV, KC><<<(unsigned)grid, kDenseWaves * 64, 0, stream>>>(Q, user_rows, items, B,   \
+                                                                                  n_items, d, apply_sigmoid, \
+                                                                                  scores, n_ug, split_items); \
+    else                                                                                                   \
+        score_dense_kernel<DTV, KC><<<(unsigned)grid, kDenseWaves * 64, 0, stream>>>(Q, user_rows, items, B, \
+                                                                                     n_items, d, apply_sigmoid, \
+                                                                                     scores, n_ug, split_items)
 #define LGX_SD_ALL(DTV)                  \
     switch (kch) {                       \
         case 2: LGX_SD(DTV, 2); break;   \
