@@ -114,7 +114,7 @@ __global__ __launch_bounds__(kStratThreads) void strat_select_kernel(const int8_
                                                                     const int32_t* __restrict__ hist, int n_bins,
                                                                     const int32_t* __restrict__ targets, uint64_t seed,
                                                                     int32_t* __restrict__ out, int out_stride,
-                                                                    int32_t* __restrict__ out_count) {
+                                                                    int32_t* __restrict__ out_count, int force_exact) {
     // per (label, 8-bit digit) counts of the exact radix path; the fast path keeps its candidates
     // (keys, items, labels) in the same bytes
     __shared__ __attribute__((aligned(16))) uint32_t dh[kMaxFolds * 256];
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(kStratThreads) void strat_select_kernel(const int8_
     }
     __syncthreads();
     if (tid == 0) {
-        int ok = n_cand <= kMaxCand;
+        int ok = n_cand <= kMaxCand && !force_exact;
         for (int l = 0; l < n_bins; ++l) ok &= need[l] <= 0 || cand_l[l] >= need[l];
         fast_ok = ok;
     }
@@ -313,12 +313,16 @@ extern "C" int lgx_strat_select(const int8_t* labels, int64_t n_users, int64_t n
     if (n_users == 0) return LGX_OK;
     LGX_REQUIRE(labels && hist && targets && out && out_count, LGX_ERR_INVALID_ARG, "lgx_strat_select: null pointer");
     const bool vec16 = n_items % 16 == 0 && ((uintptr_t)labels & 15) == 0;
+    // test switch: LGX_STRAT_EXACT=1 skips the cut-and-rank fast path (the radix select must pick
+    // the same sets); read per call so that one process can compare both paths
+    const char* ex = getenv("LGX_STRAT_EXACT");
+    const int force_exact = ex && atoi(ex) == 1 ? 1 : 0;
     if (vec16)
         strat_select_kernel<true><<<(unsigned)n_users, kStratThreads, 0, as_hip(stream)>>>(
-            labels, n_items, hist, n_bins, targets, seed, out, out_stride, out_count);
+            labels, n_items, hist, n_bins, targets, seed, out, out_stride, out_count, force_exact);
     else
         strat_select_kernel<false><<<(unsigned)n_users, kStratThreads, 0, as_hip(stream)>>>(
-            labels, n_items, hist, n_bins, targets, seed, out, out_stride, out_count);
+            labels, n_items, hist, n_bins, targets, seed, out, out_stride, out_count, force_exact);
     LGX_LAUNCH_CHECK();
     return LGX_OK;
 }

@@ -357,6 +357,32 @@ def test_score_dense(dtype):
     assert torch.allclose(S, ref, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("dtype,d", [(torch.bfloat16, 256), (torch.bfloat16, 512), (torch.float32, 128),
+                                     (torch.float32, 72)])
+def test_score_dense_lds_image(dtype, d):
+    """the LDS-staged path (16 / 32 / 16 chunks per row) and a padded row (f32 d=72), several 256-user
+    groups and a catalog that is not a multiple of the 32-item tile"""
+    rng = np.random.default_rng(d)
+    Q = torch.from_numpy((rng.standard_normal((600, d)) / np.sqrt(d)).astype(np.float32)).to(DEV).to(dtype)
+    items = torch.from_numpy(rng.standard_normal((2999, d)).astype(np.float32)).to(DEV).to(dtype)
+    S = lgx.score_dense(Q, items)
+    ref = (Q.float().double() @ items.float().double().T).float()
+    assert torch.allclose(S, ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("shape,ld", [((40, 40_000), 40_000), ((9, 20_001), 20_001), ((33, 5000), 7001)])
+def test_topk_rows_long_strided_rows(shape, ld):
+    """4 waves per row (>= 16 K columns), 4-B loads (odd widths) and a row stride above the width"""
+    rng = np.random.default_rng(ld)
+    full = rng.standard_normal((shape[0], ld)).astype(np.float32)
+    full[0, 1000:1100] = 50.0  # ties at the top -> lowest indices
+    S = torch.from_numpy(full).to(DEV)[:, :shape[1]]
+    idx, val = lgx.topk_rows(S, 20)
+    oidx, oval = oracle.topk_rows(np.ascontiguousarray(full[:, :shape[1]]), 20)
+    assert np.array_equal(idx.cpu().numpy(), oidx)
+    assert np.array_equal(val.cpu().numpy(), oval)
+
+
 def test_topk_rows_vs_oracle():
     rng = np.random.default_rng(0)
     S = rng.standard_normal((300, 7000)).astype(np.float32)

@@ -118,3 +118,27 @@ def test_create_candidates_stratification_dropin(tmp_path):
         assert len(cand[u]) == 300 and cand[u][-3:] == test[u]
         assert not np.isin(cand[u][:-3], train[u]).any()
     assert os.path.exists(root / "s" / "rec" / "3" / "candidate.npy")
+
+
+def test_fast_select_equals_radix_select(monkeypatch):
+    """the cut-and-rank fast path picks exactly the sets (and order) of the exact radix select:
+    long rows (fast path taken), a tiny label (cut = everything), and a row whose candidates
+    overflow the fast path's buffer (falls back inside the same launch)"""
+    rng = np.random.default_rng(21)
+    U, I = 6, 48_000
+    lab_h = rng.integers(0, 11, (U, I)).astype(np.int8)
+    lab_h[:, rng.choice(I, 500, replace=False)] = -1          # train items
+    lab_h[1, :] = np.where(lab_h[1] >= 0, 3, -1)              # one label only
+    lab_h[2, rng.choice(I, 7, replace=False)] = 10            # label 10 nearly empty in row 2
+    lab_h[2, lab_h[2] == 10] = 9
+    lab_h[2, :7] = 10
+    hist_h = np.stack([np.bincount(r[r >= 0], minlength=11) for r in lab_h]).astype(np.int32)
+    lab = torch.from_numpy(lab_h).to(DEV)
+    hist = torch.from_numpy(hist_h).to(DEV)
+    targets = [1000, 1000, 900, 37, 1024, 1]
+    fast = _select(lab, hist, targets, seed=12345, stride=1024)
+    monkeypatch.setenv("LGX_STRAT_EXACT", "1")
+    exact = _select(lab, hist, targets, seed=12345, stride=1024)
+    assert np.array_equal(fast[1], exact[1])
+    for u in range(U):
+        assert np.array_equal(fast[0][u, :fast[1][u]], exact[0][u, :exact[1][u]])
