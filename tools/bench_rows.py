@@ -239,6 +239,79 @@ def row_f2(rows, reps):
          "algorithmic: 12 B row out + ~6 probes of 4 B (positive draw + binary search) per row")
 
 
+def _bpr_step_cpu(G, user_w, item_w, opt, users, pos, neg, K, decay):
+    """One minibatch of the reference's BPR step on the host, restated with its own torch calls:
+    computer() (model.py:145-177) + bpr_loss (model.py:186-209) + utils.BPRLoss.stageOne (Adam)."""
+    all_emb = torch.cat([user_w, item_w])
+    embs = [all_emb]
+    for _ in range(K):
+        all_emb = torch.sparse.mm(G, all_emb)
+        embs.append(all_emb)
+    out = torch.mean(torch.stack(embs, dim=1), dim=1)
+    U = user_w.shape[0]
+    ue, pe, ne = out[:U][users], out[U:][pos], out[U:][neg]
+    reg = 0.5 * (user_w[users].norm(2).pow(2) + item_w[pos].norm(2).pow(2) + item_w[neg].norm(2).pow(2)) / len(users)
+    loss = torch.mean(torch.nn.functional.softplus((ue * ne).sum(1) - (ue * pe).sum(1))) + decay * reg
+    opt.zero_grad()
+    loss.backward()
+    opt.step()
+
+
+def row_f2b(rows, reps, tmpdir):
+    """One BPR training epoch (Procedure.BPR_train_original, Procedure.py:26-57) on the Gowalla-shaped
+    graph (BASELINE configs[0]: 29,858 x 40,981, 810,128 edges, K=3, d=64 fp32, batch 2048)."""
+    from factors_of_serendipity_recommendation_amd import train as lgx_train
+    from factors_of_serendipity_recommendation_amd.dataloader import Loader
+    from factors_of_serendipity_recommendation_amd.model import LightGCN
+    cfg = CONFIGS["gowalla"]
+    u, i = synth_edges(cfg, 2020, DEV)
+    u, i = u.cpu().numpy(), i.cpu().numpy()
+    path = os.path.join(tmpdir, "rows_gowalla")
+    os.makedirs(path, exist_ok=True)
+    order = np.argsort(u, kind="stable")
+    u, i = u[order], i[order]
+    bounds = np.searchsorted(u, np.arange(cfg.n_users + 1))
+    with open(os.path.join(path, "train.txt"), "w") as f:
+        for x in range(cfg.n_users):
+            if bounds[x + 1] > bounds[x]:
+                f.write(str(x) + " " + " ".join(map(str, i[bounds[x]:bounds[x + 1]])) + "\n")
+    with open(os.path.join(path, "test.txt"), "w") as f:
+        f.write(f"0 {int(i[0])}\n")
+    ds = Loader(path=path, device=DEV, cache_adj=False)
+    conf = {"latent_dim_rec": cfg.d, "lightGCN_n_layers": cfg.K, "keep_prob": 0.6, "A_split": False,
+            "pretrain": 0, "dropout": 0, "decay": 1e-4, "lr": 0.001}
+    torch.manual_seed(0)
+    model = LightGCN(conf, ds).to(DEV)
+    bpr = lgx_train.BPRLoss(model, conf)
+    lgx_train.BPR_train_original(ds, model, bpr, 0, batch_size=2048, device=DEV)  # warm-up epoch
+    ms = gpu_ms(lambda: lgx_train.BPR_train_original(ds, model, bpr, 1, batch_size=2048, device=DEV),
+                max(1, reps // 2))
+    E = ds.trainDataSize
+    n_batches = E // 2048 + 1
+    A = model._csr
+    nnz, N, d = A.nnz, cfg.n_users + cfg.n_items, cfg.d
+    spmm_bytes = nnz * (8 + 4 * d) + N * d * 4 + 8 * (N + 1)
+    # CPU: the reference's minibatch on the host (torch.sparse.mm COO, 16 threads), a few batches
+    from oracle.torch_ref import coo_from_csr
+    torch.set_num_threads(CPU_THREADS)
+    G = coo_from_csr(A.indptr.cpu().numpy(), A.indices.cpu().numpy(), A.vals.cpu().numpy(), N)
+    uw = torch.nn.Parameter(torch.randn(cfg.n_users, d) * 0.1)
+    iw = torch.nn.Parameter(torch.randn(cfg.n_items, d) * 0.1)
+    opt = torch.optim.Adam([uw, iw], lr=0.001)
+    rng = np.random.default_rng(0)
+    nb = 8
+    bu = [torch.from_numpy(rng.integers(0, cfg.n_users, 2048)) for _ in range(nb)]
+    bp = [torch.from_numpy(rng.integers(0, cfg.n_items, 2048)) for _ in range(nb)]
+    bn = [torch.from_numpy(rng.integers(0, cfg.n_items, 2048)) for _ in range(nb)]
+    _bpr_step_cpu(G, uw, iw, opt, bu[0], bp[0], bn[0], cfg.K, 1e-4)
+    s = cpu_s(lambda: [_bpr_step_cpu(G, uw, iw, opt, bu[j], bp[j], bn[j], cfg.K, 1e-4) for j in range(nb)])
+    emit(rows, "f2b BPR training epoch (lgx_sample_bpr + 2K lgx_propagate_layer per minibatch + torch Adam)", ms, E,
+         "train edges/s", "hbm", n_batches * 2 * cfg.K * spmm_bytes, nb * 2048, s,
+         f"{nb} minibatches of 2048 on the host: torch.sparse.mm x K + mean + BPR loss + Adam (model.py:145-209), "
+         "sampling excluded", CPU_THREADS,
+         f"{n_batches} minibatches per epoch; algorithmic = the 2K f32 SpMM layers of every minibatch")
+
+
 # ------------------------------------------------------------------------------------------ (f) 3
 def row_f3(rows, reps, tmpdir):
     """The uid item item ... train.txt parser (dataloader.py:247-277) on the device."""
@@ -317,6 +390,7 @@ def main():
     steps = [("a2", lambda r: row_a2(r, args.reps)), ("a6", lambda r: row_a6_a9(r, args.reps)),
              ("a10", lambda r: row_a10(r, args.reps)), ("a12", lambda r: row_a12(r, args.reps)),
              ("f1", lambda r: row_f1(r, args.reps)), ("f2", lambda r: row_f2(r, args.reps)),
+             ("f2b", lambda r: row_f2b(r, args.reps, tmpdir)),
              ("f3", lambda r: row_f3(r, args.reps, tmpdir)), ("f4", lambda r: row_f4(r, args.reps))]
     rows = []
     failed = []
