@@ -14,7 +14,7 @@ import factors_of_serendipity_recommendation_amd as lgx  # noqa: E402
 from factors_of_serendipity_recommendation_amd import ops  # noqa: E402
 
 
-def run(B, n_items=1_000_000, d=256, k=20, masked=True, reps=3):
+def run(B, n_items=int(os.environ.get("ABL_ITEMS", "1000000")), d=256, k=20, masked=True, reps=3):
     items = lgx.fill_normal((n_items, d), 1 / 16, 1, dtype=torch.bfloat16)
     Q = lgx.fill_normal((B, d), 1 / 16, 2, dtype=torch.bfloat16)
     mask = None
@@ -30,7 +30,7 @@ def run(B, n_items=1_000_000, d=256, k=20, masked=True, reps=3):
     t = (time.perf_counter() - t0) / reps
     tf = 2 * B * n_items * d / t / 1e12
     tag = os.path.basename(os.environ.get("LGX_LIB", "liblgx.so"))
-    print(f"{tag} B={B} masked={masked} ablate={os.environ.get('LGX_SCORE_ABLATE', '0')}: {t * 1e3:.1f} ms  {tf:.0f} TF/s",
+    print(f"{tag} I={n_items} B={B} masked={masked} ablate={os.environ.get('LGX_SCORE_ABLATE', '0')}: {t * 1e3:.1f} ms  {tf:.0f} TF/s",
           flush=True)
 
 
