@@ -60,6 +60,11 @@ SIGNATURES = {
     "lgx_parse_lines_count": (_c_int, [_vp, _c_i64, _vp, ctypes.c_size_t, _vp, _vp]),
     "lgx_parse_lines_fill": (_c_int, [_vp, _c_i64, _vp, ctypes.c_size_t, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp]),
     "lgx_sample_bpr": (_c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, _c_int, ctypes.c_uint64, _vp, _vp]),
+    "lgx_bpr_loss_workspace": (_c_int, [_c_i64, _sz_p]),
+    "lgx_bpr_loss_forward": (_c_int, [_vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp,
+                                      _vp, ctypes.c_size_t, _vp]),
+    "lgx_bpr_loss_backward": (_c_int, [_vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp,
+                                       _vp, _vp, _vp, _vp]),
     "lgx_list_dot_reduce": (_c_int, [_vp, _c_i64, _c_int, _c_i64, _vp, _vp, _vp, _vp, _c_int, _vp, _vp]),
     "lgx_layer_epilogue": (_c_int, [_vp, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_float, _vp]),
     "lgx_propagate_workspace": (_c_int, [_c_i64, _c_i64, _c_int, _sz_p]),

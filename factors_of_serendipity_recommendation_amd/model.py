@@ -16,6 +16,8 @@ Differences, all documented in DESIGN.md:
     recomputes the full K-layer propagation for every 100-user test batch, model.py:180);
   * getUsersRating returns sigmoid scores from the HIP MFMA kernel (not differentiable: the
     reference only calls it under torch.no_grad(), Procedure.py:109,127).
+  * bpr_loss runs as two fused HIP kernels (lgx_bpr_loss_forward/backward) on f32 tables;
+    bpr_loss_torch keeps the reference's torch-op form as the parity reference.
 """
 from __future__ import annotations
 
@@ -45,6 +47,27 @@ class _Propagate(torch.autograd.Function):
 
 def propagate_autograd(E0: torch.Tensor, A: CSRGraph, K: int, A_T: Optional[CSRGraph] = None) -> torch.Tensor:
     return _Propagate.apply(E0, A, K, A_T)
+
+
+class _BPRLoss(torch.autograd.Function):
+    """bpr_loss (model.py:196-209) as two fused HIP kernels (csrc/bpr.hip): forward reads each
+    triple's 3 propagated and 3 ego rows once; backward adds the row gradients into dense [N, d]
+    tables -- the propagated one then flows into _Propagate.backward."""
+
+    @staticmethod
+    def forward(ctx, light, ego_user, ego_item, users, pos, neg):
+        loss, reg, coef = ops.bpr_loss_forward(light, ego_user, ego_item, users, pos, neg)
+        ctx.save_for_backward(light, ego_user, ego_item, users, pos, neg, coef)
+        return loss, reg
+
+    @staticmethod
+    def backward(ctx, g_loss, g_reg):
+        light, ego_user, ego_item, users, pos, neg, coef = ctx.saved_tensors
+        z = torch.zeros((), dtype=torch.float32, device=light.device)
+        g_light, g_user, g_item = ops.bpr_loss_backward(light, ego_user, ego_item, users, pos, neg, coef,
+                                                        z if g_loss is None else g_loss,
+                                                        z if g_reg is None else g_reg)
+        return g_light, g_user, g_item, None, None, None
 
 
 def _graph_to_csr(G, dataset, n_users: int, n_items: int) -> CSRGraph:
@@ -109,8 +132,8 @@ class LightGCN(BasicModel):
         GT = torch.sparse_coo_tensor(torch.stack([cols, rows]), vals, (N, N)).coalesce()
         return from_sparse_coo(G, A.n_users, A.n_items), from_sparse_coo(GT, A.n_users, A.n_items)
 
-    def computer(self):
-        """propagate methods for lightGCN (model.py:145-177) on the HIP engine."""
+    def _light_out(self) -> torch.Tensor:
+        """The propagated [U+I, d] table (model.py:145-177) on the HIP engine."""
         users_emb = self.embedding_user.weight
         items_emb = self.embedding_item.weight
         use_cache = (not self.training) and not torch.is_grad_enabled()
@@ -123,10 +146,13 @@ class LightGCN(BasicModel):
         else:
             A, A_T = self._csr, None
         light_out = propagate_autograd(all_emb, A, self.n_layers, A_T)
-        users, items = torch.split(light_out, [self.num_users, self.num_items])
         if use_cache:
-            self._eval_cache = (key, (users, items))
-        return users, items
+            self._eval_cache = (key, light_out)
+        return light_out
+
+    def computer(self):
+        """propagate methods for lightGCN (model.py:145-177): (users, items) views of one table."""
+        return torch.split(self._light_out(), [self.num_users, self.num_items])
 
     def getUsersRating(self, users):
         all_users, all_items = self.computer()
@@ -143,6 +169,16 @@ class LightGCN(BasicModel):
         return users_emb, pos_emb, neg_emb, users_emb_ego, pos_emb_ego, neg_emb_ego
 
     def bpr_loss(self, users, pos, neg):
+        """model.py:196-209.  f32 tables go through the fused kernels (_BPRLoss); other dtypes
+        through the reference's torch ops (bpr_loss_torch)."""
+        light = self._light_out()
+        w_u, w_i = self.embedding_user.weight, self.embedding_item.weight
+        if light.dtype == w_u.dtype == w_i.dtype == torch.float32 and light.is_contiguous():
+            return _BPRLoss.apply(light, w_u, w_i, users, pos, neg)
+        return self.bpr_loss_torch(users, pos, neg)
+
+    def bpr_loss_torch(self, users, pos, neg):
+        """The reference's bpr_loss in torch ops (model.py:196-209), kept as the parity reference."""
         (users_emb, pos_emb, neg_emb, userEmb0, posEmb0, negEmb0) = self.getEmbedding(users.long(), pos.long(),
                                                                                       neg.long())
         reg_loss = (1 / 2) * (userEmb0.norm(2).pow(2) + posEmb0.norm(2).pow(2) +

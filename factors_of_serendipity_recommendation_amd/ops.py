@@ -263,3 +263,56 @@ def fill_normal(shape, std: float, seed: int, dtype=torch.float32, device="cuda"
     _lib.check(_lib.lib().lgx_fill_normal(t.data_ptr(), t.numel(), float(std), int(seed) & (2**64 - 1),
                                           _dtype_code(t), _stream_ptr(t.device)), "lgx_fill_normal")
     return t
+
+
+# ------------------------------------------------------------------------------------ BPR loss
+def _bpr_args(light, ego_user, ego_item, users, pos, neg):
+    require_gpu(light, ego_user, ego_item, users, pos, neg)
+    for t in (light, ego_user, ego_item):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("light / ego tables must be contiguous float32")
+    U, I = ego_user.shape[0], ego_item.shape[0]
+    d = light.shape[1]
+    if light.shape[0] != U + I or ego_user.shape[1] != d or ego_item.shape[1] != d:
+        raise ValueError(f"shape mismatch: light {tuple(light.shape)}, ego {tuple(ego_user.shape)} / "
+                         f"{tuple(ego_item.shape)}")
+    idx = [t.contiguous().long() for t in (users, pos, neg)]
+    if not (idx[0].shape == idx[1].shape == idx[2].shape) or idx[0].dim() != 1 or idx[0].numel() == 0:
+        raise ValueError("users / pos / neg must be equal-length non-empty 1-D index tensors")
+    return U, I, d, idx
+
+
+def bpr_loss_forward(light: torch.Tensor, ego_user: torch.Tensor, ego_item: torch.Tensor, users: torch.Tensor,
+                     pos: torch.Tensor, neg: torch.Tensor):
+    """``lgx_bpr_loss_forward`` (model.py:196-209): returns (loss, reg_loss, coef) -- two 0-dim f32
+    tensors and the per-triple sigmoid(<u,n> - <u,p>) the backward needs.  light = the propagated
+    [U+I, d] table, ego_* = the embedding weights."""
+    U, I, d, (u, p, n) = _bpr_args(light, ego_user, ego_item, users, pos, neg)
+    B = u.numel()
+    sz = ctypes.c_size_t()
+    _lib.check(_lib.lib().lgx_bpr_loss_workspace(B, ctypes.byref(sz)), "lgx_bpr_loss_workspace")
+    ws = torch.empty(sz.value, dtype=torch.uint8, device=light.device)
+    coef = torch.empty(B, dtype=torch.float32, device=light.device)
+    loss = torch.empty((), dtype=torch.float32, device=light.device)
+    reg = torch.empty((), dtype=torch.float32, device=light.device)
+    _lib.check(_lib.lib().lgx_bpr_loss_forward(light.data_ptr(), ego_user.data_ptr(), ego_item.data_ptr(), U, I, d,
+                                               u.data_ptr(), p.data_ptr(), n.data_ptr(), B, coef.data_ptr(),
+                                               loss.data_ptr(), reg.data_ptr(), ws.data_ptr(), sz.value,
+                                               _stream_ptr(light.device)), "lgx_bpr_loss_forward")
+    return loss, reg, coef
+
+
+def bpr_loss_backward(light, ego_user, ego_item, users, pos, neg, coef, grad_loss, grad_reg):
+    """``lgx_bpr_loss_backward``: dense gradients (g_light [U+I, d], g_user [U, d], g_item [I, d]) of
+    grad_loss * loss + grad_reg * reg (0-dim device tensors)."""
+    U, I, d, (u, p, n) = _bpr_args(light, ego_user, ego_item, users, pos, neg)
+    g_light = torch.zeros_like(light)
+    g_user = torch.zeros_like(ego_user)
+    g_item = torch.zeros_like(ego_item)
+    gl = grad_loss.to(torch.float32).contiguous()
+    gr = grad_reg.to(torch.float32).contiguous()
+    _lib.check(_lib.lib().lgx_bpr_loss_backward(light.data_ptr(), ego_user.data_ptr(), ego_item.data_ptr(), U, I, d,
+                                                u.data_ptr(), p.data_ptr(), n.data_ptr(), u.numel(), coef.data_ptr(),
+                                                gl.data_ptr(), gr.data_ptr(), g_light.data_ptr(), g_user.data_ptr(),
+                                                g_item.data_ptr(), _stream_ptr(light.device)), "lgx_bpr_loss_backward")
+    return g_light, g_user, g_item

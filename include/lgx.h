@@ -28,6 +28,7 @@
  *   lgx_parse_lines_*      Loader / Data file parsing            code/dataloader.py:247-277; load_data.py:27-48
  *   lgx_strat_labels/select create_candidates_stratification   recommend.py:314-452
  *   lgx_sample_bpr         sample_negative / sample_negative_ByUser   sources/sampling.cpp:27-86
+ *   lgx_bpr_loss_*         LightGCN.bpr_loss + its backward        code/model.py:196-209; utils.py:43-52
  *   lgx_list_dot_reduce    difference / ser1 / ser2 / diversity per-user list products
  *                          recommend.py:305-307; utils.py:34-35, 117-121, 265-267
  */
@@ -239,6 +240,24 @@ int lgx_parse_lines_fill(const uint8_t* text, int64_t n_bytes, const void* ws, s
 int lgx_sample_bpr(const int64_t* pos_indptr, const int32_t* pos_items, int64_t n_users, int64_t n_items,
                    const int32_t* users, int64_t n_rows, int64_t per_user, int neg_num, uint64_t seed,
                    int32_t* out, lgx_stream_t stream);
+
+/*
+ * BPR minibatch loss (model.py:196-209) fused.  light [n_users + n_items, d] f32 = the propagated
+ * table (users first); ego_user [n_users, d] / ego_item [n_items, d] f32 = the embedding weights;
+ * users / pos / neg int64 [B].  forward writes *out_loss = mean softplus(<u,n> - <u,p>),
+ * *out_reg = 0.5 (|U0|^2 + |P0|^2 + |N0|^2) / B, and coef[b] = sigmoid(<u,n> - <u,p>) for backward.
+ * An out-of-range index makes the loss NaN.  backward ADDS into g_light / g_user / g_item (dense,
+ * caller-zeroed) the gradients of (*grad_loss) * loss + (*grad_reg) * reg (scalars on the device).
+ */
+int lgx_bpr_loss_workspace(int64_t B, size_t* ws_bytes);
+int lgx_bpr_loss_forward(const float* light, const float* ego_user, const float* ego_item, int64_t n_users,
+                         int64_t n_items, int64_t d, const int64_t* users, const int64_t* pos, const int64_t* neg,
+                         int64_t B, float* coef, float* out_loss, float* out_reg, void* ws, size_t ws_bytes,
+                         lgx_stream_t stream);
+int lgx_bpr_loss_backward(const float* light, const float* ego_user, const float* ego_item, int64_t n_users,
+                          int64_t n_items, int64_t d, const int64_t* users, const int64_t* pos, const int64_t* neg,
+                          int64_t B, const float* coef, const float* grad_loss, const float* grad_reg, float* g_light,
+                          float* g_user, float* g_item, lgx_stream_t stream);
 
 /* ---------------------------------------------------------------- 8(f) rank 1: list x list similarity */
 #define LGX_REDUCE_MAX 0

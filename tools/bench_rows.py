@@ -286,6 +286,10 @@ def row_f2b(rows, reps, tmpdir):
     lgx_train.BPR_train_original(ds, model, bpr, 0, batch_size=2048, device=DEV)  # warm-up epoch
     ms = gpu_ms(lambda: lgx_train.BPR_train_original(ds, model, bpr, 1, batch_size=2048, device=DEV),
                 max(1, reps // 2))
+    model.bpr_loss = model.bpr_loss_torch  # A/B: the reference's torch-op loss in the same epoch
+    ms_torch_loss = gpu_ms(lambda: lgx_train.BPR_train_original(ds, model, bpr, 2, batch_size=2048, device=DEV),
+                           max(1, reps // 2))
+    del model.bpr_loss
     E = ds.trainDataSize
     n_batches = E // 2048 + 1
     A = model._csr
@@ -305,11 +309,12 @@ def row_f2b(rows, reps, tmpdir):
     bn = [torch.from_numpy(rng.integers(0, cfg.n_items, 2048)) for _ in range(nb)]
     _bpr_step_cpu(G, uw, iw, opt, bu[0], bp[0], bn[0], cfg.K, 1e-4)
     s = cpu_s(lambda: [_bpr_step_cpu(G, uw, iw, opt, bu[j], bp[j], bn[j], cfg.K, 1e-4) for j in range(nb)])
-    emit(rows, "f2b BPR training epoch (lgx_sample_bpr + 2K lgx_propagate_layer per minibatch + torch Adam)", ms, E,
+    emit(rows, "f2b BPR training epoch (lgx_sample_bpr + 2K lgx_propagate_layer + lgx_bpr_loss_* per minibatch + torch Adam)", ms, E,
          "train edges/s", "hbm", n_batches * 2 * cfg.K * spmm_bytes, nb * 2048, s,
          f"{nb} minibatches of 2048 on the host: torch.sparse.mm x K + mean + BPR loss + Adam (model.py:145-209), "
          "sampling excluded", CPU_THREADS,
-         f"{n_batches} minibatches per epoch; algorithmic = the 2K f32 SpMM layers of every minibatch")
+         f"{n_batches} minibatches per epoch; algorithmic = the 2K f32 SpMM layers of every minibatch; "
+         f"with the torch-op loss instead of lgx_bpr_loss_*: {ms_torch_loss:.1f} ms")
 
 
 # ------------------------------------------------------------------------------------------ (f) 3
