@@ -286,6 +286,9 @@ def row_f2b(rows, reps, tmpdir):
     lgx_train.BPR_train_original(ds, model, bpr, 0, batch_size=2048, device=DEV)  # warm-up epoch
     ms = gpu_ms(lambda: lgx_train.BPR_train_original(ds, model, bpr, 1, batch_size=2048, device=DEV),
                 max(1, reps // 2))
+    if os.environ.get("LGX_ROWS_F2B_FUSED_ONLY"):  # profiling: only the product epochs
+        print(f"f2b epoch {ms:.1f} ms", flush=True)
+        return
     model.bpr_loss = model.bpr_loss_torch  # A/B: the reference's torch-op loss in the same epoch
     ms_torch_loss = gpu_ms(lambda: lgx_train.BPR_train_original(ds, model, bpr, 2, batch_size=2048, device=DEV),
                            max(1, reps // 2))
