@@ -65,6 +65,8 @@ SIGNATURES = {
                                       _vp, ctypes.c_size_t, _vp]),
     "lgx_bpr_loss_backward": (_c_int, [_vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp,
                                        _vp, _vp, _vp, _vp]),
+    "lgx_adam_step": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                               ctypes.c_double, _c_i64, _vp]),
     "lgx_list_dot_reduce": (_c_int, [_vp, _c_i64, _c_int, _c_i64, _vp, _vp, _vp, _vp, _c_int, _vp, _vp]),
     "lgx_layer_epilogue": (_c_int, [_vp, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_float, _vp]),
     "lgx_propagate_workspace": (_c_int, [_c_i64, _c_i64, _c_int, _sz_p]),

@@ -11,9 +11,47 @@ from __future__ import annotations
 import time
 
 import torch
-from torch import optim
 
-from . import sampling
+from . import _lib, sampling
+from .graph import _stream_ptr, require_gpu
+
+
+class Adam(torch.optim.Optimizer):
+    """torch.optim.Adam as BPRLoss uses it (code/utils.py:41: lr only; betas (0.9, 0.999), eps 1e-8,
+    no weight decay, no amsgrad), one ``lgx_adam_step`` launch per parameter instead of torch's
+    ~7 multi-tensor passes.  State keys match torch's (step, exp_avg, exp_avg_sq), so a
+    state_dict round-trips.  GPU f32 parameters only -- there is no CPU path."""
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                require_gpu(p)
+                if p.dtype != torch.float32 or not p.is_contiguous() or p.grad.is_sparse:
+                    raise TypeError("lgx Adam takes dense contiguous float32 parameters")
+                st = self.state[p]
+                if not st:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                g = p.grad.contiguous()
+                _lib.check(_lib.lib().lgx_adam_step(p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(),
+                                                    st["exp_avg_sq"].data_ptr(), p.numel(), float(group["lr"]),
+                                                    float(b1), float(b2), float(group["eps"]),
+                                                    int(st["step"].item()), _stream_ptr(p.device)),
+                           "lgx_adam_step")
+        return loss
 
 
 class BPRLoss:
@@ -23,7 +61,7 @@ class BPRLoss:
         self.model = recmodel
         self.weight_decay = config["decay"]
         self.lr = config["lr"]
-        self.opt = optim.Adam(recmodel.parameters(), lr=self.lr)
+        self.opt = Adam(recmodel.parameters(), lr=self.lr)
 
     def stageOne(self, users, pos, neg) -> float:
         loss, reg_loss = self.model.bpr_loss(users, pos, neg)

@@ -29,6 +29,7 @@
  *   lgx_strat_labels/select create_candidates_stratification   recommend.py:314-452
  *   lgx_sample_bpr         sample_negative / sample_negative_ByUser   sources/sampling.cpp:27-86
  *   lgx_bpr_loss_*         LightGCN.bpr_loss + its backward        code/model.py:196-209; utils.py:43-52
+ *   lgx_adam_step          BPRLoss's torch.optim.Adam step          code/utils.py:41,50
  *   lgx_list_dot_reduce    difference / ser1 / ser2 / diversity per-user list products
  *                          recommend.py:305-307; utils.py:34-35, 117-121, 265-267
  */
@@ -258,6 +259,14 @@ int lgx_bpr_loss_backward(const float* light, const float* ego_user, const float
                           int64_t n_items, int64_t d, const int64_t* users, const int64_t* pos, const int64_t* neg,
                           int64_t B, const float* coef, const float* grad_loss, const float* grad_reg, float* g_light,
                           float* g_user, float* g_item, lgx_stream_t stream);
+
+/*
+ * One torch.optim.Adam step (code/utils.py:41: no weight decay, no amsgrad) over n f32 elements in
+ * one pass: exp_avg / exp_avg_sq updated in place, param -= lr/(1-beta1^step) * m / (sqrt(v)/sqrt(1-beta2^step) + eps).
+ * All four arrays 16-byte aligned; step >= 1 is the step count after this update.
+ */
+int lgx_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, double lr,
+                  double beta1, double beta2, double eps, int64_t step, lgx_stream_t stream);
 
 /* ---------------------------------------------------------------- 8(f) rank 1: list x list similarity */
 #define LGX_REDUCE_MAX 0

@@ -164,3 +164,31 @@ def test_model_bpr_loss_fused_equals_reference_form(mlls):
     assert abs(l1 - l2) <= 1e-5 * abs(l2) and abs(r1 - r2) <= 1e-5 * abs(r2)
     for a, b in ((gu1, gu2), (gi1, gi2)):
         assert (a - b).abs().max().item() <= 1e-5 * b.abs().max().item()
+
+
+@pytest.mark.parametrize("n", [4 * 70_839 * 16, 1001])
+def test_lgx_adam_matches_torch_adam(n):
+    """train.Adam (one lgx_adam_step pass) against torch.optim.Adam(lr) over 6 steps: parameters and
+    both moments within fp32 rounding (1e-6 relative, 1e-6 of the tensor's scale absolute -- a
+    moment near a zero crossing keeps the rounding of its inputs), the updates to 1e-4 relative;
+    an odd length exercises the tail."""
+    from factors_of_serendipity_recommendation_amd import train
+    g = torch.Generator().manual_seed(n)
+    p0 = torch.randn(n, generator=g).to(DEV)
+    grads = [torch.randn(n, generator=g).to(DEV) * s for s in (1.0, 0.1, 0.0, 3.0, 1e-3, 1.0)]
+    a = torch.nn.Parameter(p0.clone())
+    b = torch.nn.Parameter(p0.clone())
+    oa, ob = train.Adam([a], lr=1e-3), torch.optim.Adam([b], lr=1e-3)
+    for gr in grads:
+        a.grad, b.grad = gr.clone(), gr.clone()
+        oa.step()
+        ob.step()
+    for x, y in ((a, b), (oa.state[a]["exp_avg"], ob.state[b]["exp_avg"]),
+                 (oa.state[a]["exp_avg_sq"], ob.state[b]["exp_avg_sq"])):
+        x, y = x.detach(), y.detach()
+        assert torch.allclose(x, y, rtol=1e-6, atol=1e-6 * y.abs().max().item())
+    # the parameter updates themselves (~6e-3): equal to 1e-4 relative, plus the few ulps of |p|
+    # that 6 roundings of p itself leave (1e-6 |p| = 8 ulps)
+    da, db = a.detach() - p0, b.detach() - p0
+    assert ((da - db).abs() <= 1e-4 * db.abs() + 1e-6 * p0.abs() + 1e-9).all()
+    assert float(oa.state[a]["step"]) == 6.0

@@ -312,7 +312,7 @@ def row_f2b(rows, reps, tmpdir):
     bn = [torch.from_numpy(rng.integers(0, cfg.n_items, 2048)) for _ in range(nb)]
     _bpr_step_cpu(G, uw, iw, opt, bu[0], bp[0], bn[0], cfg.K, 1e-4)
     s = cpu_s(lambda: [_bpr_step_cpu(G, uw, iw, opt, bu[j], bp[j], bn[j], cfg.K, 1e-4) for j in range(nb)])
-    emit(rows, "f2b BPR training epoch (lgx_sample_bpr + 2K lgx_propagate_layer + lgx_bpr_loss_* per minibatch + torch Adam)", ms, E,
+    emit(rows, "f2b BPR training epoch (lgx_sample_bpr + 2K lgx_propagate_layer + lgx_bpr_loss_* + lgx_adam_step per minibatch)", ms, E,
          "train edges/s", "hbm", n_batches * 2 * cfg.K * spmm_bytes, nb * 2048, s,
          f"{nb} minibatches of 2048 on the host: torch.sparse.mm x K + mean + BPR loss + Adam (model.py:145-209), "
          "sampling excluded", CPU_THREADS,
