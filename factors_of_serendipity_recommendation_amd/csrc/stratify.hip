@@ -50,9 +50,14 @@ __global__ __launch_bounds__(kStratThreads) void strat_labels_kernel(const float
                                                                     const int32_t* __restrict__ mask_indices,
                                                                     int8_t* __restrict__ labels,
                                                                     int32_t* __restrict__ hist) {
+    // per-thread counters (column = thread: conflict-free, no atomics) -- one LDS atomic per item on
+    // ~10 hot bins serialised the whole row; summed into h after the sweep
+    __shared__ uint32_t hp[kMaxFolds * kStratThreads];
     __shared__ int32_t h[kMaxFolds];
     const int64_t u = blockIdx.x;
-    if (threadIdx.x < kMaxFolds) h[threadIdx.x] = 0;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int b = 0; b < kMaxFolds; ++b) hp[b * kStratThreads + tid] = 0;
     __syncthreads();
     const float* s = scores + u * n_items;
     int8_t* lab = labels + u * n_items;
@@ -73,10 +78,10 @@ __global__ __launch_bounds__(kStratThreads) void strat_labels_kernel(const float
                 if (q >= n4) break;
                 const int l0 = label_of(v[j].x, min16, inter16, num_fold), l1 = label_of(v[j].y, min16, inter16, num_fold);
                 const int l2 = label_of(v[j].z, min16, inter16, num_fold), l3 = label_of(v[j].w, min16, inter16, num_fold);
-                atomicAdd(&h[l0], 1);
-                atomicAdd(&h[l1], 1);
-                atomicAdd(&h[l2], 1);
-                atomicAdd(&h[l3], 1);
+                hp[l0 * kStratThreads + tid] += 1;
+                hp[l1 * kStratThreads + tid] += 1;
+                hp[l2 * kStratThreads + tid] += 1;
+                hp[l3 * kStratThreads + tid] += 1;
                 reinterpret_cast<uint32_t*>(lab)[q] = (uint32_t)(l0 & 255) | ((uint32_t)(l1 & 255) << 8) |
                                                       ((uint32_t)(l2 & 255) << 16) | ((uint32_t)(l3 & 255) << 24);
             }
@@ -84,9 +89,15 @@ __global__ __launch_bounds__(kStratThreads) void strat_labels_kernel(const float
     } else {
         for (int64_t i = threadIdx.x; i < n_items; i += kStratThreads) {
             const int lv = label_of(s[i], min16, inter16, num_fold);
-            atomicAdd(&h[lv], 1);
+            hp[lv * kStratThreads + tid] += 1;
             lab[i] = (int8_t)lv;
         }
+    }
+    __syncthreads();
+    if (tid < kMaxFolds) {
+        uint32_t c = 0;
+        for (int t = 0; t < kStratThreads; ++t) c += hp[tid * kStratThreads + ((t + tid) & (kStratThreads - 1))];
+        h[tid] = (int32_t)c;
     }
     __syncthreads();  // the row's labels (global) and counts are complete before the mask fix-up
     if (mask_indptr) {
