@@ -11,10 +11,10 @@
 //   utils.diversity_sub    mean over the list itself     (utils.py:265-267) -- sum / (|A| |B|)
 //
 // MI355X design: one 256-thread workgroup per user, its 4 waves striding over 32-entry blocks of A.
-// A block's 32 rows are the MFMA B operand, held in VGPRs; B's rows stream through in 32-row tiles
-// as the A operand (gathered 16-B chunks straight from HBM/L2 -- lists are short, the tables are
-// L2/MALL resident at the reference's sizes), so each lane ends a tile holding 16 products of ONE
-// entry of A and reduces them in registers.  fp32: v_mfma_f32_32x32x2_f32 (the exact fp32 fmaf
+// A block's 32 rows are the MFMA B operand, held in VGPRs; B's rows are the A operand in 32-row
+// tiles, staged once per user into a padded LDS image when they fit in 48 KB (every block of A
+// reads them; 2.25 -> 1.73 ms on the f1 row) and gathered per block from HBM/L2 otherwise, so each
+// lane ends a tile holding 16 products of ONE entry of A and reduces them in registers.  fp32: v_mfma_f32_32x32x2_f32 (the exact fp32 fmaf
 // chain); bf16: v_mfma_f32_32x32x16_bf16 with fp32 accumulation.
 #include "lgx_common.h"
 
@@ -65,6 +65,7 @@ struct RowFrag<LGX_DTYPE_BF16> {
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 constexpr int kListWaves = 4;
+constexpr int kListLdsBytes = 32 * 1024;  // B-list image: 5 workgroups (20 waves) per CU
 
 template <int DT, int KCH, bool MAX>
 __global__ __launch_bounds__(256) void list_dot_reduce_kernel(const void* __restrict__ table, int64_t d,
@@ -74,11 +75,59 @@ __global__ __launch_bounds__(256) void list_dot_reduce_kernel(const void* __rest
                                                              const int32_t* __restrict__ b_items,
                                                              float* __restrict__ out) {
     typedef RowFrag<DT> F;
+    // B image in LDS: row r, chunk c, half h at 16-B slot r * RS + 2c + h; the odd row stride RS
+    // puts the 32 rows of a fragment read on distinct bank quads (conflict-free ds_read_b128)
+    constexpr int RS = 2 * KCH + 1;
+    constexpr int kMaxTiles = kListLdsBytes / (32 * RS * 16);
+    __shared__ uint4 bimg[kMaxTiles > 0 ? kMaxTiles * 32 * RS : 1];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, col = lane & 31;
     const int64_t u = blockIdx.x;
     const int64_t a0 = a_indptr[u], a1 = a_indptr[u + 1];
     const int64_t b0 = b_indptr[u], b1 = b_indptr[u + 1];
+    const int64_t nbt = (b1 - b0 + 31) / 32;
+    if (a1 > a0 && nbt > 0 && nbt <= kMaxTiles) {
+        // the user's B rows are read by every block of A: stage them once (zero rows past |B|)
+        for (int64_t i = threadIdx.x; i < nbt * 32 * 2 * KCH; i += 256) {
+            const int64_t r = i / (2 * KCH);
+            const int ch = (int)(i % (2 * KCH));
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (b0 + r < b1) {
+                const typename F::chunk c = F::load(table, b_items[b0 + r], d, ch >> 1, ch & 1, true);
+                v = __builtin_bit_cast(uint4, c);
+            }
+            bimg[r * RS + ch] = v;
+        }
+        __syncthreads();
+        for (int64_t blk = a0 + (int64_t)wave * 32; blk < a1; blk += kListWaves * 32) {
+            const int64_t p = blk + col;
+            const bool ok = p < a1;
+            const int64_t arow = ok ? a_items[p] : 0;
+            typename F::chunk af[KCH];
+#pragma unroll
+            for (int c = 0; c < KCH; ++c) af[c] = F::load(table, arow, d, c, h, ok);
+            float red = MAX ? -INFINITY : 0.0f;
+            for (int64_t t = 0; t < nbt; ++t) {
+                const uint4* brow = bimg + (t * 32 + col) * RS + h;
+                f32x16 acc;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+                for (int c = 0; c < KCH; ++c)
+                    acc = F::mma(__builtin_bit_cast(typename F::chunk, brow[2 * c]), af[c], acc);
+                const int64_t t0 = b0 + t * 32;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    if (t0 + acc_row(r, h) < b1) red = MAX ? fmaxf(red, acc[r]) : red + acc[r];
+                }
+            }
+            const float other = __shfl_xor(red, 32, 64);
+            red = MAX ? fmaxf(red, other) : red + other;
+            if (h == 0 && ok) out[p] = red;
+        }
+        return;
+    }
+    // |B| beyond the LDS image (or empty): B tiles gathered from global memory per block of A
     for (int64_t blk = a0 + (int64_t)wave * 32; blk < a1; blk += kListWaves * 32) {
         const int64_t p = blk + col;  // this lane's entry of A (column of the product tile)
         const bool ok = p < a1;
