@@ -84,16 +84,9 @@ __device__ __forceinline__ bool in_list(const int32_t* t, int64_t n, int32_t x) 
 }
 
 // evaluate_foldout.h:16-112 per user; float accumulators with double increments as in the C++.
-__global__ void foldout_kernel(const int32_t* __restrict__ rankings, int64_t users, int k,
-                               const int64_t* __restrict__ truth_indptr,
-                               const int32_t* __restrict__ truth_indices,
-                               const double* __restrict__ inv_log2, float* __restrict__ results) {
-    const int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (u >= users) return;
-    const int32_t* rank = rankings + u * k;
-    const int32_t* truth = truth_indices + truth_indptr[u];
-    const int64_t tl = truth_indptr[u + 1] - truth_indptr[u];
-    float* out = results + u * 5 * (int64_t)k;
+// out[c * ostride + i] for curve c (precision, recall, map, ndcg, mrr) at rank i.
+__device__ __forceinline__ void foldout_user(const int32_t* rank, const int32_t* truth, int64_t tl, int k,
+                                             const double* __restrict__ inv_log2, float* out) {
     int hits = 0;
     float sum_pre = 0.0f, dcg = 0.0f, idcg = 0.0f;
     bool found = false;
@@ -118,6 +111,48 @@ __global__ void foldout_kernel(const int32_t* __restrict__ rankings, int64_t use
             out[4 * k + i] = 0.0f;
         }
     }
+}
+
+__global__ void foldout_kernel(const int32_t* __restrict__ rankings, int64_t users, int k,
+                               const int64_t* __restrict__ truth_indptr,
+                               const int32_t* __restrict__ truth_indices,
+                               const double* __restrict__ inv_log2, float* __restrict__ results) {
+    const int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (u >= users) return;
+    const int64_t t0 = truth_indptr[u];
+    foldout_user(rankings + u * k, truth_indices + t0, truth_indptr[u + 1] - t0, k, inv_log2,
+                 results + u * 5 * (int64_t)k);
+}
+
+// k <= kFoldStagedK: the block's 64 ranking rows come in and its 64 x 5k result rows go out as
+// contiguous coalesced runs through LDS (odd row strides: conflict-free per-thread rows); a thread
+// per user writing its own 5k-float row directly was a strided store per element (1.77 ms for
+// 1 M users at k=20).
+constexpr int kFoldUsers = 64;
+constexpr int kFoldStagedK = 64;
+
+__global__ __launch_bounds__(kFoldUsers) void foldout_staged_kernel(const int32_t* __restrict__ rankings,
+                                                                   int64_t users, int k,
+                                                                   const int64_t* __restrict__ truth_indptr,
+                                                                   const int32_t* __restrict__ truth_indices,
+                                                                   const double* __restrict__ inv_log2,
+                                                                   float* __restrict__ results) {
+    extern __shared__ float fold_sm[];
+    const int S = 5 * k + 1, RK = k | 1;
+    float* oimg = fold_sm;
+    int32_t* rimg = reinterpret_cast<int32_t*>(fold_sm + kFoldUsers * S);
+    const int64_t u0 = blockIdx.x * (int64_t)kFoldUsers;
+    const int nu = (int)min((int64_t)kFoldUsers, users - u0);
+    const int t = threadIdx.x;
+    for (int i = t; i < nu * k; i += kFoldUsers) rimg[(i / k) * RK + i % k] = rankings[u0 * k + i];
+    __syncthreads();
+    if (t < nu) {
+        const int64_t a = truth_indptr[u0 + t];
+        foldout_user(rimg + t * RK, truth_indices + a, truth_indptr[u0 + t + 1] - a, k, inv_log2, oimg + t * S);
+    }
+    __syncthreads();
+    const int W = 5 * k;
+    for (int i = t; i < nu * W; i += kFoldUsers) results[u0 * W + i] = oimg[(i / W) * S + i % W];
 }
 
 }  // namespace
@@ -152,8 +187,14 @@ extern "C" int lgx_foldout_metrics(const int32_t* rankings, int64_t users, int k
     if (users == 0) return LGX_OK;
     LGX_REQUIRE(rankings && truth_indptr && inv_log2 && results, LGX_ERR_INVALID_ARG,
                 "lgx_foldout_metrics: null pointer");
-    foldout_kernel<<<ceil_div(users, 128), 128, 0, as_hip(stream)>>>(rankings, users, k, truth_indptr,
-                                                                      truth_indices, inv_log2, results);
+    if (k <= kFoldStagedK) {
+        const size_t lds = (size_t)kFoldUsers * ((5 * k + 1) * sizeof(float) + (k | 1) * sizeof(int32_t));
+        foldout_staged_kernel<<<(unsigned)ceil_div(users, (int64_t)kFoldUsers), kFoldUsers, lds, as_hip(stream)>>>(
+            rankings, users, k, truth_indptr, truth_indices, inv_log2, results);
+    } else {
+        foldout_kernel<<<ceil_div(users, 128), 128, 0, as_hip(stream)>>>(rankings, users, k, truth_indptr,
+                                                                          truth_indices, inv_log2, results);
+    }
     LGX_LAUNCH_CHECK();
     return LGX_OK;
 }

@@ -402,6 +402,19 @@ def test_foldout_metrics_bit_exact(mlls):
     assert np.array_equal(got.cpu().numpy(), mlls["oracle_curves"])
 
 
+@pytest.mark.parametrize("k,users", [(1, 5), (7, 130), (20, 1000), (64, 65), (65, 70), (100, 3)])
+def test_foldout_metrics_k_sweep(k, users):
+    """Both kernels (LDS-staged for k <= 64, direct above) bit-exact vs the oracle, with user counts
+    that leave a partial last block, hit-free users and truth lists longer than k."""
+    rng = np.random.default_rng(k * 1000 + users)
+    n_items = 3 * k + 50
+    rankings = np.stack([rng.permutation(n_items)[:k] for _ in range(users)]).astype(np.int32)
+    truths = [list(rng.choice(n_items, size=int(rng.integers(1, 2 * k + 2)), replace=False)) for _ in range(users)]
+    truths[0] = [n_items + 5]  # never ranked
+    got = ops.foldout_metrics(torch.from_numpy(rankings).to(DEV), ops.lists_to_device_csr(truths, DEV, sort=False))
+    assert np.array_equal(got.cpu().numpy(), oracle.evaluate_foldout(rankings, truths))
+
+
 def test_eval_score_matrix_foldout_dropin():
     rng = np.random.default_rng(2)
     S = rng.standard_normal((64, 3000)).astype(np.float32)
