@@ -11,7 +11,8 @@
 // numbers and '\n' ends a line, so "\r\n" endings, trailing spaces and a missing final newline are
 // accepted.  Values must fit int32 (larger ones saturate).  Lines with no number are skipped.
 //
-// Layout: 64-KiB chunks (one 256-thread workgroup, 256 bytes per thread).  Pass 1 counts the
+// Layout: 64-KiB chunks (one 256-thread workgroup, 256 bytes per thread), staged in LDS by
+// coalesced loads (per-thread byte walks over global memory ran at 25 GB/s).  Pass 1 counts the
 // numbers and line-first numbers of every chunk; one workgroup scans the chunk counts (64-bit
 // offsets: files beyond 2^31 bytes are fine); pass 2 recounts per thread, scans inside the
 // workgroup and writes every number at its global position.  A number belongs to the chunk that
@@ -27,12 +28,46 @@ constexpr int64_t kChunkBytes = kParseThreads * kBytesPerThread;
 
 __device__ __forceinline__ bool is_digit(uint8_t c) { return c >= '0' && c <= '9'; }
 
-__device__ __forceinline__ bool starts_number(const uint8_t* __restrict__ t, int64_t i) {
+// The workgroup's 64-KiB chunk staged in LDS by coalesced 16-B loads, each thread's 256-B range
+// padded by 16 B so that the threads' byte walks fall on different banks; bytes outside the
+// chunk (a number's tail in the next chunk, the look-back before it) come from global memory.
+constexpr int kSegPad = 16;
+constexpr int kChunkLds = (int)(kChunkBytes + (kChunkBytes / kBytesPerThread) * kSegPad);
+
+struct Text {
+    const uint8_t* __restrict__ g;
+    const uint8_t* s;  // LDS image of [lo, hi)
+    int64_t lo, hi;
+    __device__ __forceinline__ uint8_t operator[](int64_t i) const {
+        if (i >= lo && i < hi) {
+            const int64_t o = i - lo;
+            return s[o + (o / kBytesPerThread) * kSegPad];
+        }
+        return g[i];
+    }
+};
+
+__device__ Text stage_chunk(const uint8_t* __restrict__ g, int64_t n, uint8_t* img) {
+    const int64_t lo = min((int64_t)blockIdx.x * kChunkBytes, n), hi = min(lo + kChunkBytes, n);
+    if (hi - lo == kChunkBytes && ((uintptr_t)g & 15) == 0) {
+        for (int q = threadIdx.x; q < (int)(kChunkBytes / 16); q += kParseThreads) {
+            const uint4 v = reinterpret_cast<const uint4*>(g + lo)[q];
+            const int o = q * 16;
+            *reinterpret_cast<uint4*>(img + o + (o / kBytesPerThread) * kSegPad) = v;
+        }
+    } else {
+        for (int64_t o = threadIdx.x; o < hi - lo; o += kParseThreads) img[o + (o / kBytesPerThread) * kSegPad] = g[lo + o];
+    }
+    __syncthreads();
+    return Text{g, img, lo, hi};
+}
+
+__device__ __forceinline__ bool starts_number(const Text& t, int64_t i) {
     return is_digit(t[i]) && (i == 0 || !is_digit(t[i - 1]));
 }
 
 // the number starting at i is the first of its line: nothing but separators back to '\n' or the start
-__device__ __forceinline__ bool first_of_line(const uint8_t* __restrict__ t, int64_t i) {
+__device__ __forceinline__ bool first_of_line(const Text& t, int64_t i) {
     for (int64_t j = i - 1; j >= 0; --j) {
         const uint8_t c = t[j];
         if (c == '\n') return true;
@@ -41,7 +76,7 @@ __device__ __forceinline__ bool first_of_line(const uint8_t* __restrict__ t, int
     return true;
 }
 
-__device__ __forceinline__ int32_t parse_number(const uint8_t* __restrict__ t, int64_t i, int64_t n) {
+__device__ __forceinline__ int32_t parse_number(const Text& t, int64_t i, int64_t n) {
     int64_t v = 0;
     for (; i < n && is_digit(t[i]); ++i) {
         v = v * 10 + (t[i] - '0');
@@ -54,7 +89,7 @@ struct ThreadCounts {
     int64_t numbers, firsts;
 };
 
-__device__ __forceinline__ ThreadCounts count_range(const uint8_t* __restrict__ t, int64_t lo, int64_t hi) {
+__device__ __forceinline__ ThreadCounts count_range(const Text& t, int64_t lo, int64_t hi) {
     ThreadCounts c{0, 0};
     for (int64_t i = lo; i < hi; ++i) {
         if (starts_number(t, i)) {
@@ -86,8 +121,10 @@ __global__ __launch_bounds__(kParseThreads) void parse_count_kernel(const uint8_
                                                                    int64_t* __restrict__ chunk_numbers,
                                                                    int64_t* __restrict__ chunk_firsts) {
     __shared__ int64_t sh[kParseThreads];
+    __shared__ __attribute__((aligned(16))) uint8_t img[kChunkLds];
+    const Text tx = stage_chunk(t, n, img);
     const int64_t lo = blockIdx.x * kChunkBytes + threadIdx.x * kBytesPerThread;
-    const ThreadCounts c = count_range(t, min(lo, n), min(lo + kBytesPerThread, n));
+    const ThreadCounts c = count_range(tx, min(lo, n), min(lo + kBytesPerThread, n));
     int64_t dummy;
     const int64_t tn = block_exclusive_scan(c.numbers, sh, &dummy);
     const int64_t tf = block_exclusive_scan(c.firsts, sh, &dummy);
@@ -126,18 +163,20 @@ __global__ __launch_bounds__(kParseThreads) void parse_fill_kernel(const uint8_t
                                                                   int64_t* __restrict__ line_ptr,
                                                                   int32_t* __restrict__ items) {
     __shared__ int64_t sh[kParseThreads];
+    __shared__ __attribute__((aligned(16))) uint8_t img[kChunkLds];
+    const Text tx = stage_chunk(t, n, img);
     const int64_t lo = min(blockIdx.x * kChunkBytes + threadIdx.x * kBytesPerThread, n);
     const int64_t hi = min(lo + kBytesPerThread, n);
-    const ThreadCounts c = count_range(t, lo, hi);
+    const ThreadCounts c = count_range(tx, lo, hi);
     int64_t num_off, first_off;
     block_exclusive_scan(c.numbers, sh, &num_off);
     block_exclusive_scan(c.firsts, sh, &first_off);
     int64_t tok = chunk_numbers[blockIdx.x] + num_off;      // global index of this thread's next number
     int64_t lines = chunk_firsts[blockIdx.x] + first_off;   // line-first numbers before it
     for (int64_t i = lo; i < hi; ++i) {
-        if (!starts_number(t, i)) continue;
-        const int32_t v = parse_number(t, i, n);
-        if (first_of_line(t, i)) {
+        if (!starts_number(tx, i)) continue;
+        const int32_t v = parse_number(tx, i, n);
+        if (first_of_line(tx, i)) {
             line_user[lines] = v;
             line_ptr[lines] = tok - lines;  // items before this line
             ++lines;
