@@ -13,7 +13,7 @@
 namespace lgx {
 namespace {
 
-constexpr int kUnroll = 2;
+constexpr int kUnroll = 4;
 
 // WPR waves per row (4 for long rows, 1 for short ones: 4 rows per workgroup).  VEC: rows are
 // 16-B aligned, so each lane loads float4s (1 KB per wave instruction).  Per batch of loads one
