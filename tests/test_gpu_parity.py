@@ -141,6 +141,25 @@ def test_propagation_dims_and_depths(d, K):
     assert_prop_close(out, oracle.propagate(ip, ix, iv, E0, K), np.abs(E0).max())
 
 
+@pytest.mark.parametrize("d", [8, 64, 256, 1024])
+def test_propagation_many_partials_per_row(d):
+    """seg_len 2 splits every row of degree > 2 into up to hundreds of partials: the fix-up's 16
+    (or 4, at d=1024) groups per workgroup each sum a strided share, then one group adds them."""
+    U, I, E = 300, 200, 9000
+    u, i = random_graph(U, I, E, 40 + d)
+    ip, ix, iv = oracle.build_norm_adj(u, i, U, I)
+    A = lgx.from_csr_arrays(ip, ix, iv, device=DEV, seg_len=2)
+    assert int(np.diff(ip).max()) > 64  # some row has more than 32 partials
+    E0 = (np.random.default_rng(d).standard_normal((U + I, d)) * 0.1).astype(np.float32)
+    out = lgx.propagate(A, torch.from_numpy(E0).to(DEV), 3).cpu().numpy()
+    assert_prop_close(out, oracle.propagate(ip, ix, iv, E0, 3), np.abs(E0).max())
+    if d % 8 == 0:  # bf16 storage through the same fix-up
+        Eb = _bf16_round(E0)
+        outb = lgx.propagate(A, torch.from_numpy(Eb).to(DEV).to(torch.bfloat16), 3).cpu().numpy()
+        ref = oracle.propagate(ip, ix, iv, Eb, 3)
+        assert (np.abs(outb - ref) <= 2e-2 * np.abs(ref) + 2e-2 * np.sqrt(np.mean(ref ** 2))).all()
+
+
 def test_spmm_plain_matches_oracle():
     U, I, E = 800, 900, 20000
     u, i = random_graph(U, I, E, 3)
