@@ -69,7 +69,7 @@ def test_choose_seg_len_range():
     assert choose_seg_len(0) == 64
     assert choose_seg_len(2_000_000) == 64
     assert choose_seg_len(1_000_000_000) == 8192
-    assert choose_seg_len(100_000_000) == 2048
+    assert choose_seg_len(100_000_000) == 4096
 
 
 def test_balanced_bounds():
