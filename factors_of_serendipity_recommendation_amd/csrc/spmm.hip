@@ -319,7 +319,13 @@ int dispatch_layer(const LayerArgs& a, hipStream_t stream) {
     const int64_t chunks = a.d / VEC;
     if (chunks <= 4) return launch_layer<T, 4, 1>(a, stream);
     if (chunks <= 8) return launch_layer<T, 8, 1>(a, stream);
-    if (chunks <= 16) return launch_layer<T, 16, 1>(a, stream);
+    if (chunks <= 16) {
+        // short segments (the plan of an L2/MALL-resident graph, graph.choose_seg_len): 8 gathers
+        // in flight per lane and more waves per SIMD beat 16 (tools/segprobe.py: ML-1M 37.8 ->
+        // 35.8 us, Amazon-book shape 144.3 -> 126.6 us per layer); C4-sized plans keep 16
+        if (a.seg_len <= 128) return launch_layer<T, 16, 1, 8>(a, stream);
+        return launch_layer<T, 16, 1>(a, stream);
+    }
     if (chunks <= 32) return launch_layer<T, 32, 1>(a, stream);
     if (chunks <= 64) return launch_layer<T, 64, 1>(a, stream);
     if (chunks <= 128) return launch_layer<T, 64, 2>(a, stream);

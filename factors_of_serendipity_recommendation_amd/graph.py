@@ -21,19 +21,25 @@ import torch
 
 from . import _lib
 
-# Target number of row segments per launch (tools/segprobe.py, one MI355X, SpMM layer time by
-# seg_len): Gowalla shape 64 -> 38.3 us (32: 41.7, 128: 39.3); ML-1M 32/64/128 within 3 %;
-# Amazon-book shape 256 -> 146.8 us against 151.7 at 128; C4 stays at the 8192 cap.
-_TARGET_SEGMENTS = 32768
+# Segment plans (tools/segprobe.py, one MI355X, SpMM layer time by seg_len and gathers in flight):
+#  - graphs under 2^24 nnz (tables L2/MALL-resident): ~64 K segments of 32..128 nonzeros, run with
+#    8 gathers in flight per lane (csrc/spmm.hip picks that for seg_len <= 128): Gowalla shape 37.8
+#    -> 36.9 us, ML-1M 37.8 -> 35.8 us, Amazon-book shape 144.3 -> 126.6 us per layer;
+#  - larger graphs: ~32 K segments of 64..8192 with 16 in flight (C4: 8192, 29.9 ms per layer against
+#    30.7 at 2048 and 30.6 at 16384, tools/spmm_probe.py --phase).
+_SMALL_NNZ = 1 << 24
 
 
 def choose_seg_len(nnz: int) -> int:
     """Segment length: long enough to amortise the fix-up, short enough that hub rows are split
-    into >= the chip's group slots (power of two in [64, 8192]; the C4 layer takes 29.9 ms at 8192
-    against 30.7 at 2048 and 30.6 at 16384, tools/spmm_probe.py --phase)."""
-    want = max(1, nnz // _TARGET_SEGMENTS)
-    s = 64
-    while s < want and s < 8192:
+    into >= the chip's group slots (power of two; see the table above)."""
+    if nnz < _SMALL_NNZ:
+        target, lo, hi = 65536, 32, 128
+    else:
+        target, lo, hi = 32768, 256, 8192
+    want = max(1, nnz // target)
+    s = lo
+    while s < want and s < hi:
         s *= 2
     return s
 

@@ -66,10 +66,12 @@ def test_make_plan_phases(seg_len):
 
 
 def test_choose_seg_len_range():
-    assert choose_seg_len(0) == 64
-    assert choose_seg_len(2_000_000) == 64
+    assert choose_seg_len(0) == 32
+    assert choose_seg_len(1_620_256) == 32    # Gowalla shape
+    assert choose_seg_len(5_968_216) == 128   # Amazon-book shape
     assert choose_seg_len(1_000_000_000) == 8192
     assert choose_seg_len(100_000_000) == 4096
+    assert choose_seg_len(1 << 24) == 512     # large-graph plans never take the short-segment kernel
 
 
 def test_balanced_bounds():
