@@ -22,6 +22,7 @@ LGX_DTYPE_F32 = 0
 LGX_DTYPE_BF16 = 1
 LGX_LAYER_PLAIN, LGX_LAYER_FIRST, LGX_LAYER_MID, LGX_LAYER_LAST, LGX_LAYER_ONLY, LGX_LAYER_PARTIAL = range(6)
 LGX_REDUCE_MAX, LGX_REDUCE_SUM = 0, 1
+LGX_STRAT_EXACT = 1
 
 _c_i64 = ctypes.c_int64
 _c_int = ctypes.c_int
@@ -56,6 +57,8 @@ SIGNATURES = {
     "lgx_spmm_csr": (_c_int, [ctypes.POINTER(LgxCSR), _vp, _vp, _c_i64, _c_int, _vp]),
     "lgx_strat_labels": (_c_int, [_vp, _c_i64, _c_i64, _c_float, _c_float, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "lgx_strat_select": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_int, _vp, ctypes.c_uint64, _vp, _c_int, _vp, _vp]),
+    "lgx_strat_select_ex": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_int, _vp, ctypes.c_uint64, _vp, _c_int, _vp,
+                                     _c_int, _vp]),
     "lgx_parse_lines_workspace": (_c_int, [_c_i64, _sz_p]),
     "lgx_parse_lines_count": (_c_int, [_vp, _c_i64, _vp, ctypes.c_size_t, _vp, _vp]),
     "lgx_parse_lines_fill": (_c_int, [_vp, _c_i64, _vp, ctypes.c_size_t, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp]),
@@ -77,7 +80,7 @@ SIGNATURES = {
                                 _c_int, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "lgx_topk_rows": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _c_int, _vp, _vp, _vp]),
     "lgx_foldout_metrics": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _vp, _vp, _vp]),
-    "lgx_gather_scores": (_c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp]),
+    "lgx_gather_scores": (_c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp]),
     "lgx_synth_edges": (_c_int, [ctypes.c_uint64, _vp, _c_i64, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp]),
     "lgx_fill_normal": (_c_int, [_vp, _c_i64, ctypes.c_float, ctypes.c_uint64, _c_int, _vp]),
 }

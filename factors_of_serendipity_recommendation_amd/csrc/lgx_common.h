@@ -38,6 +38,7 @@ void set_error(const char* fmt, ...);
 inline hipStream_t as_hip(lgx_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 constexpr int kWave = 64;  // CDNA wavefront
+constexpr int kMaxTopK = 256;  // largest k of the top-k entry points (WaveList<4>)
 
 // ------------------------------------------------------------------ bf16 <-> f32
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) {

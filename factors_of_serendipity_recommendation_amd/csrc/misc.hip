@@ -22,7 +22,7 @@ namespace {
 // (user, candidate) pair, G = d/4 (f32 rows read as 16-B chunks), reduced with xor-shuffles.
 template <int G>
 __global__ __launch_bounds__(256) void gather_scores_kernel(const float* __restrict__ eu, const float* __restrict__ ei,
-                                                            int64_t n_users, int64_t d,
+                                                            int64_t n_users, int64_t n_items, int64_t d,
                                                             const int64_t* __restrict__ cand_indptr,
                                                             const int32_t* __restrict__ cand_items,
                                                             int64_t n_pairs, float* __restrict__ out) {
@@ -35,8 +35,13 @@ __global__ __launch_bounds__(256) void gather_scores_kernel(const float* __restr
         const int64_t mid = (lo + hi) >> 1;
         if (cand_indptr[mid + 1] <= p) lo = mid + 1; else hi = mid;
     }
+    const int64_t item = cand_items[p];
+    if (item < 0 || item >= n_items) {  // never read outside the item table (the host raises first)
+        if (gl == 0) out[p] = __builtin_nanf("");
+        return;
+    }
     const float* a = eu + lo * d;
-    const float* b = ei + (int64_t)cand_items[p] * d;
+    const float* b = ei + item * d;
     float s = 0.0f;
     for (int64_t off = (int64_t)gl * 4; off < d; off += 4 * G) {
         const float4 x = *reinterpret_cast<const float4*>(a + off);
@@ -54,7 +59,7 @@ __global__ __launch_bounds__(256) void gather_scores_kernel(const float* __restr
 // reduction as gather_scores_kernel, so the scores are bit-identical.
 template <int G, int CH, int U>
 __global__ __launch_bounds__(256) void gather_scores_by_user(const float* __restrict__ eu, const float* __restrict__ ei,
-                                                             int64_t n_users, int64_t d,
+                                                             int64_t n_users, int64_t n_items, int64_t d,
                                                              const int64_t* __restrict__ cand_indptr,
                                                              const int32_t* __restrict__ cand_items,
                                                              float* __restrict__ out) {
@@ -71,15 +76,18 @@ __global__ __launch_bounds__(256) void gather_scores_by_user(const float* __rest
     }
     for (int64_t pb = p0 + grp; pb < p1; pb += (int64_t)GPW * U) {
         float4 y[U][CH];
+        bool ok[U];
 #pragma unroll
         for (int j = 0; j < U; ++j) {
             const int64_t q = pb + (int64_t)j * GPW;
-            const float* b = ei + (q < p1 ? (int64_t)cand_items[q] : 0) * d;
+            const int64_t item = q < p1 ? (int64_t)cand_items[q] : 0;
+            ok[j] = item >= 0 && item < n_items;  // never read outside the item table
+            const float* b = ei + (ok[j] ? item : 0) * d;
 #pragma unroll
             for (int c = 0; c < CH; ++c) {
                 const int64_t off = (int64_t)(gl + c * G) * 4;
-                y[j][c] = (q < p1 && off < d) ? *reinterpret_cast<const float4*>(b + off)
-                                              : make_float4(0.f, 0.f, 0.f, 0.f);
+                y[j][c] = (q < p1 && ok[j] && off < d) ? *reinterpret_cast<const float4*>(b + off)
+                                                       : make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
 #pragma unroll
@@ -94,7 +102,7 @@ __global__ __launch_bounds__(256) void gather_scores_by_user(const float* __rest
             }
 #pragma unroll
             for (int m = G >> 1; m > 0; m >>= 1) s += __shfl_xor(s, m, G);
-            if (gl == 0 && q < p1) out[q] = s;
+            if (gl == 0 && q < p1) out[q] = ok[j] ? s : __builtin_nanf("");
         }
     }
 }
@@ -154,11 +162,11 @@ extern "C" int lgx_device_info(int device, int* cu_count, int* xcd_count, char* 
     return LGX_OK;
 }
 
-extern "C" int lgx_gather_scores(const float* emb_user, const float* emb_item, int64_t n_users, int64_t d,
-                                   const int64_t* cand_indptr, const int32_t* cand_items, int64_t n_pairs,
+extern "C" int lgx_gather_scores(const float* emb_user, const float* emb_item, int64_t n_users, int64_t n_items,
+                                   int64_t d, const int64_t* cand_indptr, const int32_t* cand_items, int64_t n_pairs,
                                    float* scores, lgx_stream_t stream_) {
     hipStream_t stream = as_hip(stream_);
-    LGX_REQUIRE(emb_user && emb_item && cand_indptr && scores && n_users >= 0 && n_pairs >= 0,
+    LGX_REQUIRE(emb_user && emb_item && cand_indptr && scores && n_users >= 0 && n_items > 0 && n_pairs >= 0,
                 LGX_ERR_INVALID_ARG, "lgx_gather_scores: bad arguments");
     LGX_REQUIRE(d > 0 && d % 4 == 0, LGX_ERR_UNSUPPORTED, "lgx_gather_scores: d must be a multiple of 4");
     if (n_pairs == 0) return LGX_OK;
@@ -166,7 +174,8 @@ extern "C" int lgx_gather_scores(const float* emb_user, const float* emb_item, i
     if (chunks <= 64 * 4) {  // by user: one wave per user
         const unsigned grid = (unsigned)ceil_div(n_users * 64, 256);
 #define LGX_GU(GV, CHV, UV) \
-    gather_scores_by_user<GV, CHV, UV><<<grid, 256, 0, stream>>>(emb_user, emb_item, n_users, d, cand_indptr, cand_items, scores)
+    gather_scores_by_user<GV, CHV, UV><<<grid, 256, 0, stream>>>(emb_user, emb_item, n_users, n_items, d, cand_indptr, \
+                                                                cand_items, scores)
         if (chunks <= 4) LGX_GU(4, 1, 4);
         else if (chunks <= 8) LGX_GU(8, 1, 4);
         else if (chunks <= 16) LGX_GU(16, 1, 4);
@@ -180,7 +189,7 @@ extern "C" int lgx_gather_scores(const float* emb_user, const float* emb_item, i
     }
 #define LGX_GS(GV)                                                                                      \
     gather_scores_kernel<GV><<<ceil_div(n_pairs * GV, 256), 256, 0, stream>>>(emb_user, emb_item, n_users, \
-                                                                              d, cand_indptr, cand_items, \
+                                                                              n_items, d, cand_indptr, cand_items, \
                                                                               n_pairs, scores)
     if (chunks <= 4) LGX_GS(4);
     else if (chunks <= 8) LGX_GS(8);

@@ -54,9 +54,10 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kWavesPerBlock = 4;
 constexpr int kUsersPerWave = 32;
-constexpr int kUsersPerBlock = kWavesPerBlock * kUsersPerWave;
+// waves per workgroup of the register-fragment kernel: its per-user lists live in LDS (k keys per
+// user), so the largest k run one wave per workgroup
+__host__ __device__ constexpr int v1_waves(int k) { return k <= 128 ? 4 : 1; }
 
 // ---------------------------------------------------------------------------- fragments
 // f32: chunk c of lane half h = features [8c + 4h, 8c + 4h + 4) -> k-steps 4c..4c+3
@@ -545,8 +546,8 @@ struct WaveTopK {
 };
 
 
-template <int DT, int KCH, bool MINMAX>
-__global__ __launch_bounds__(256) void score_topk_kernel(ScoreArgs a) {
+template <int DT, int KCH, bool MINMAX, int WPB>
+__global__ __launch_bounds__(WPB * 64) void score_topk_kernel(ScoreArgs a) {
     typedef Frag<DT> F;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -554,7 +555,7 @@ __global__ __launch_bounds__(256) void score_topk_kernel(ScoreArgs a) {
     const int k = a.k;
     uint64_t* lk = reinterpret_cast<uint64_t*>(smem + (size_t)wave * list_bytes_per_wave(k));
 
-    const int64_t b = (int64_t)blockIdx.x * kUsersPerBlock + wave * kUsersPerWave + col;  // this lane's user
+    const int64_t b = (int64_t)blockIdx.x * (WPB * kUsersPerWave) + wave * kUsersPerWave + col;  // this lane's user
     const bool user_ok = b < a.B;
     const int64_t qrow = user_ok ? (a.user_rows ? a.user_rows[b] : b) : 0;
     typename F::chunk uf[KCH];
@@ -907,7 +908,8 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
 #endif
 }
 
-// one wave per query: merge the split lists, masked tail, optional sigmoid
+// one wave per query: merge the split lists, masked tail, optional sigmoid (k <= 64 R)
+template <int R>
 __global__ __launch_bounds__(64) void score_topk_finalize(ScoreArgs a, float mask_value, int apply_sigmoid,
                                                           int32_t* __restrict__ out_idx, float* __restrict__ out_val,
                                                           float* __restrict__ minmax_out) {
@@ -917,27 +919,34 @@ __global__ __launch_bounds__(64) void score_topk_finalize(ScoreArgs a, float mas
     const int64_t total = (int64_t)a.n_splits * k;
     const float* ps = a.part_score + (size_t)b * total;
     const int32_t* pi = a.part_idx + (size_t)b * total;
-    uint64_t top = 0;
+    WaveList<R> top;
+    top.clear();
     for (int64_t base = 0; base < total; base += 64) {
         const int64_t j = base + lane;
         const uint64_t cand = (j < total && pi[j] >= 0) ? make_key(ps[j], pi[j]) : 0ull;
-        wave_topk_push(top, cand, k, lane);
+        top.push(cand, k, lane);
     }
-    const int n_real = __popcll(__ballot(top != 0ull));
-    if (lane < k) {
+    int n_real = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) n_real += __popcll(__ballot(top.t[r] != 0ull));
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = 64 * r + lane;
+        if (e >= k) continue;
+        const uint64_t key = top.t[r];
         int32_t idx = -1;
         float val = mask_value;
-        if (top) {
-            idx = key_index(top);
-            const float s = key_score(top);
+        if (key) {
+            idx = key_index(key);
+            const float s = key_score(key);
             val = apply_sigmoid ? 1.0f / (1.0f + expf(-s)) : s;
         } else if (a.mask_indptr) {
             const int64_t m0 = a.mask_indptr[b], m1 = a.mask_indptr[b + 1];
-            const int64_t j = m0 + (lane - n_real);
+            const int64_t j = m0 + (e - n_real);
             if (j < m1) idx = a.mask_indices[j];
         }
-        out_idx[b * k + lane] = idx;
-        if (out_val) out_val[b * k + lane] = val;
+        out_idx[b * k + e] = idx;
+        if (out_val) out_val[b * k + e] = val;
     }
     if (minmax_out && b == 0 && lane == 0) {
         minmax_out[0] = unord_f32(a.minmax[0]);
@@ -1165,7 +1174,7 @@ SplitPlan plan_splits(int64_t B, int64_t n_items, int dtype, int64_t d, int k) {
         const int n = (int)ceil_div(n_items, per);
         return {n, per, true, n % 8 == 0, ut, waves};
     }
-    const int64_t user_blocks = ceil_div(B, kUsersPerBlock);
+    const int64_t user_blocks = ceil_div(B, (int64_t)v1_waves(k) * kUsersPerWave);
     int64_t s = ceil_div(2048, user_blocks);                       // aim for >= ~8 workgroups per CU
     s = std::min<int64_t>(s, std::max<int64_t>(1, tiles32 / 8));  // >= 8 tiles per split
     s = std::max<int64_t>(1, std::min<int64_t>(s, 64));
@@ -1180,15 +1189,15 @@ int set_lds_limit(KernelT kernel, size_t shmem) {
     return LGX_OK;
 }
 
-template <int DT, bool MM>
-int launch_v1(const ScoreArgs& a, int kch, hipStream_t stream) {
-    const size_t shmem = (size_t)kWavesPerBlock * list_bytes_per_wave(a.k);
-    dim3 grid((unsigned)ceil_div(a.B, kUsersPerBlock), (unsigned)a.n_splits);
-#define LGX_SK(KC)                                                                     \
-    do {                                                                               \
-        int rc_ = set_lds_limit(score_topk_kernel<DT, KC, MM>, shmem);                \
-        if (rc_) return rc_;                                                           \
-        score_topk_kernel<DT, KC, MM><<<grid, 256, shmem, stream>>>(a);                \
+template <int DT, bool MM, int WPB>
+int launch_v1_waves(const ScoreArgs& a, int kch, hipStream_t stream) {
+    const size_t shmem = (size_t)WPB * list_bytes_per_wave(a.k);
+    dim3 grid((unsigned)ceil_div(a.B, (int64_t)WPB * kUsersPerWave), (unsigned)a.n_splits);
+#define LGX_SK(KC)                                                                      \
+    do {                                                                                \
+        int rc_ = set_lds_limit(score_topk_kernel<DT, KC, MM, WPB>, shmem);            \
+        if (rc_) return rc_;                                                            \
+        score_topk_kernel<DT, KC, MM, WPB><<<grid, WPB * 64, shmem, stream>>>(a);      \
     } while (0)
     switch (kch) {
         case 2: LGX_SK(2); break;
@@ -1200,6 +1209,11 @@ int launch_v1(const ScoreArgs& a, int kch, hipStream_t stream) {
 #undef LGX_SK
     LGX_LAUNCH_CHECK();
     return LGX_OK;
+}
+
+template <int DT, bool MM>
+int launch_v1(const ScoreArgs& a, int kch, hipStream_t stream) {
+    return v1_waves(a.k) == 4 ? launch_v1_waves<DT, MM, 4>(a, kch, stream) : launch_v1_waves<DT, MM, 1>(a, kch, stream);
 }
 
 // tile buffers of the LDS kernel: as many as fit beside the top-k lists in the workgroup's share of
@@ -1228,14 +1242,16 @@ int launch_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream
 
 template <int KS, bool MM, int ABL, int WAVES, int NACC>
 int launch_lds_shape(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
-    // development switches (timing studies only): LGX_SCORE_NOSTAGGER=1 runs the lockstep order,
-    // LGX_SCORE_MFMA32=1 the 32x32x16 main loop
+#ifdef LGX_DEV_SWITCHES
+    // development builds only (tools/Makefile): LGX_SCORE_NOSTAGGER=1 runs the lockstep order,
+    // LGX_SCORE_MFMA32=1 the 32x32x16 main loop; the product library never reads the environment
     static const char* ns = getenv("LGX_SCORE_NOSTAGGER");
     static const char* m32 = getenv("LGX_SCORE_MFMA32");
     if constexpr (ABL == 0 && KS == 16) {  // d = 256 (the C5 shape) only: keeps the build short
         if (m32 && m32[0] == '1') return launch_lds_kernel<KS, MM, ABL, WAVES, NACC, true, false>(a, p, stream);
         if (ns && ns[0] == '1') return launch_lds_kernel<KS, MM, ABL, WAVES, NACC, false, true>(a, p, stream);
     }
+#endif
     return launch_lds_kernel<KS, MM, ABL, WAVES, NACC, true, true>(a, p, stream);
 }
 
@@ -1326,7 +1342,7 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
     hipStream_t stream = as_hip(stream_);
     LGX_REQUIRE(B >= 0 && n_items >= 0 && out_idx, LGX_ERR_INVALID_ARG, "lgx_score_topk: bad arguments");
     LGX_REQUIRE(dtype == LGX_DTYPE_F32 || dtype == LGX_DTYPE_BF16, LGX_ERR_INVALID_ARG, "lgx_score_topk: dtype");
-    LGX_REQUIRE(k >= 1 && k <= 64, LGX_ERR_UNSUPPORTED, "lgx_score_topk: k=%d outside [1, 64]", k);
+    LGX_REQUIRE(k >= 1 && k <= kMaxTopK, LGX_ERR_UNSUPPORTED, "lgx_score_topk: k=%d outside [1, %d]", k, kMaxTopK);
     const int64_t vec = dtype == LGX_DTYPE_F32 ? 4 : 8;
     const int kch = kch_for(dtype, d);
     LGX_REQUIRE(d > 0 && d % vec == 0 && kch > 0, LGX_ERR_UNSUPPORTED,
@@ -1345,13 +1361,16 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
         LGX_LAUNCH_CHECK();
     }
     const bool mm = minmax_out != nullptr;
-    // development switches (timing studies only): LGX_SCORE_ABLATE=1 drops the top-k work,
-    // =3 keeps only its fast-path filter, =4 hides the mask from the scoring kernel
-    static const char* abl_env = getenv("LGX_SCORE_ABLATE");  // =5: =1 without the tile refills
+#ifdef LGX_DEV_SWITCHES
+    // development builds only (tools/Makefile): LGX_SCORE_ABLATE=1 drops the top-k work, =3 keeps
+    // only its fast-path filter, =4 hides the mask from the scoring kernel, =5: =1 without the tile
+    // refills.  The product library has none of these (no getenv, no ablation instantiations).
+    static const char* abl_env = getenv("LGX_SCORE_ABLATE");
     static const bool ablate = abl_env && abl_env[0] == '1';
     static const bool ablate3 = abl_env && abl_env[0] == '3';
     static const bool ablate4 = abl_env && abl_env[0] == '4';
     static const bool ablate5 = abl_env && abl_env[0] == '5';
+#endif
     const size_t esz = dtype == LGX_DTYPE_F32 ? 4 : 2;
     for (int i = 0; i < n_ranges; ++i) {
         const UserRange& R = ranges[i];
@@ -1364,22 +1383,28 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
                     mask_indptr ? mask_indptr + R.u0 : nullptr, mask_indices, k, p.n_splits, p.split_items,
                     reinterpret_cast<float*>(wsr), reinterpret_cast<int32_t*>(wsr + list_bytes), minmax};
         int rc;
+#ifdef LGX_DEV_SWITCHES
         ScoreArgs ka = a;
         if (ablate4) ka.mask_indptr = nullptr;
         if (p.lds && ablate4) rc = launch_lds<false>(ka, p, stream);
         else if (p.lds && ablate) rc = launch_lds<false, 1>(a, p, stream);
         else if (p.lds && ablate3) rc = launch_lds<false, 3>(a, p, stream);
         else if (p.lds && ablate5) rc = launch_lds<false, 5>(a, p, stream);
-        else if (p.lds) rc = mm ? launch_lds<true>(a, p, stream) : launch_lds<false>(a, p, stream);
+        else
+#endif
+        if (p.lds) rc = mm ? launch_lds<true>(a, p, stream) : launch_lds<false>(a, p, stream);
         else if (dtype == LGX_DTYPE_F32) rc = mm ? launch_v1<LGX_DTYPE_F32, true>(a, kch, stream)
                                                  : launch_v1<LGX_DTYPE_F32, false>(a, kch, stream);
         else rc = mm ? launch_v1<LGX_DTYPE_BF16, true>(a, kch, stream)
                      : launch_v1<LGX_DTYPE_BF16, false>(a, kch, stream);
         if (rc) return rc;
         // min / max is final after the last range's kernel (stream order): only its finalize reports it
-        score_topk_finalize<<<(unsigned)Bi, 64, 0, stream>>>(a, mask_value, apply_sigmoid, out_idx + R.u0 * k,
-                                                             out_val ? out_val + R.u0 * k : nullptr,
-                                                             i + 1 == n_ranges ? minmax_out : nullptr);
+        int32_t* oi = out_idx + R.u0 * k;
+        float* ov = out_val ? out_val + R.u0 * k : nullptr;
+        float* om = i + 1 == n_ranges ? minmax_out : nullptr;
+        if (k <= 64) score_topk_finalize<1><<<(unsigned)Bi, 64, 0, stream>>>(a, mask_value, apply_sigmoid, oi, ov, om);
+        else if (k <= 128) score_topk_finalize<2><<<(unsigned)Bi, 64, 0, stream>>>(a, mask_value, apply_sigmoid, oi, ov, om);
+        else score_topk_finalize<4><<<(unsigned)Bi, 64, 0, stream>>>(a, mask_value, apply_sigmoid, oi, ov, om);
         LGX_LAUNCH_CHECK();
     }
     return LGX_OK;

@@ -36,6 +36,16 @@ __device__ __forceinline__ V stream_load(const V* p) { return __builtin_nontempo
 template <typename V>
 __device__ __forceinline__ V stream_load(const V* p) { return *p; }
 #endif
+// LGX_SPMM_NT_COLD (development builds only): gathers of columns >= g_nt_cut (the cold tail of a
+// degree-ordered numbering) are non-temporal, so that they do not displace the hot rows
+#ifdef LGX_SPMM_NT_COLD
+__device__ int g_nt_cut[3] = {0x7fffffff, 0x7fffffff, 0x7fffffff};  // cold: [c0, c1) or >= c2
+typedef uint32_t nt_u32x4 __attribute__((ext_vector_type(4)));
+template <typename R>
+__device__ __forceinline__ R nt_load16(const void* p) {
+    return __builtin_bit_cast(R, __builtin_nontemporal_load(reinterpret_cast<const nt_u32x4*>(p)));
+}
+#endif
 
 template <typename T>
 struct Vec;
@@ -207,9 +217,17 @@ __global__ __launch_bounds__(kThreads) void spmm_segments(LayerArgs a) {
                 const int col = __shfl(my_col, src < n ? src : 0, G);
                 w[u] = src < n ? __shfl(my_val, src, G) : 0.0f;
                 const T* xr = X + (int64_t)col * d;
+#ifdef LGX_SPMM_NT_COLD
+                const bool cold = (col >= g_nt_cut[0] && col < g_nt_cut[1]) || col >= g_nt_cut[2];
+#endif
 #pragma unroll
                 for (int c = 0; c < CPL; ++c) {
                     const int64_t off = (int64_t)(c * G + gl) * VEC;
+#ifdef LGX_SPMM_NT_COLD
+                    if (src < n && off < d && cold)
+                        x[u][c] = nt_load16<typename Vec<T>::raw>(xr + off);
+                    else
+#endif
                     if (src < n && off < d) x[u][c] = Vec<T>::load_raw(xr + off);
                     else x[u][c] = typename Vec<T>::raw{};
                 }
@@ -488,3 +506,11 @@ extern "C" int lgx_propagate(const lgx_csr* A, const void* E0, float* out, int64
     }
     return LGX_OK;
 }
+
+#ifdef LGX_SPMM_NT_COLD
+extern "C" int lgx_dev_set_nt_cut(int c0, int c1, int c2) {
+    const int cut[3] = {c0, c1, c2};
+    LGX_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_nt_cut), cut, sizeof(cut)));
+    return LGX_OK;
+}
+#endif

@@ -327,9 +327,10 @@ extern "C" int lgx_strat_labels(const float* scores, int64_t n_users, int64_t n_
     return LGX_OK;
 }
 
-extern "C" int lgx_strat_select(const int8_t* labels, int64_t n_users, int64_t n_items, const int32_t* hist,
-                                int n_bins, const int32_t* targets, uint64_t seed, int32_t* out, int out_stride,
-                                int32_t* out_count, lgx_stream_t stream) {
+extern "C" int lgx_strat_select_ex(const int8_t* labels, int64_t n_users, int64_t n_items, const int32_t* hist,
+                                   int n_bins, const int32_t* targets, uint64_t seed, int32_t* out, int out_stride,
+                                   int32_t* out_count, int flags, lgx_stream_t stream) {
+    LGX_REQUIRE((flags & ~LGX_STRAT_EXACT) == 0, LGX_ERR_INVALID_ARG, "lgx_strat_select: unknown flags 0x%x", flags);
     LGX_REQUIRE(n_users >= 0 && n_items >= 0 && n_bins >= 1 && n_bins <= kMaxFolds && n_items < INT32_MAX,
                 LGX_ERR_INVALID_ARG, "lgx_strat_select: bad sizes (n_bins in [1, %d])", kMaxFolds);
     LGX_REQUIRE(out_stride >= 1 && out_stride <= kMaxStratK, LGX_ERR_UNSUPPORTED,
@@ -337,10 +338,8 @@ extern "C" int lgx_strat_select(const int8_t* labels, int64_t n_users, int64_t n
     if (n_users == 0) return LGX_OK;
     LGX_REQUIRE(labels && hist && targets && out && out_count, LGX_ERR_INVALID_ARG, "lgx_strat_select: null pointer");
     const bool vec16 = n_items % 16 == 0 && ((uintptr_t)labels & 15) == 0;
-    // test switch: LGX_STRAT_EXACT=1 skips the cut-and-rank fast path (the radix select must pick
-    // the same sets); read per call so that one process can compare both paths
-    const char* ex = getenv("LGX_STRAT_EXACT");
-    const int force_exact = ex && atoi(ex) == 1 ? 1 : 0;
+    // LGX_STRAT_EXACT skips the cut-and-rank fast path (the radix select must pick the same sets)
+    const int force_exact = (flags & LGX_STRAT_EXACT) ? 1 : 0;
     if (vec16)
         strat_select_kernel<true><<<(unsigned)n_users, kStratThreads, 0, as_hip(stream)>>>(
             labels, n_items, hist, n_bins, targets, seed, out, out_stride, out_count, force_exact);
@@ -349,4 +348,11 @@ extern "C" int lgx_strat_select(const int8_t* labels, int64_t n_users, int64_t n
             labels, n_items, hist, n_bins, targets, seed, out, out_stride, out_count, force_exact);
     LGX_LAUNCH_CHECK();
     return LGX_OK;
+}
+
+extern "C" int lgx_strat_select(const int8_t* labels, int64_t n_users, int64_t n_items, const int32_t* hist,
+                                int n_bins, const int32_t* targets, uint64_t seed, int32_t* out, int out_stride,
+                                int32_t* out_count, lgx_stream_t stream) {
+    return lgx_strat_select_ex(labels, n_users, n_items, hist, n_bins, targets, seed, out, out_stride, out_count, 0,
+                               stream);
 }

@@ -19,17 +19,19 @@ constexpr int kUnroll = 4;
 // 16-B aligned, so each lane loads float4s (1 KB per wave instruction).  Per batch of loads one
 // integer compare of ord(score) against the running k-th key's score bits rules out the batch
 // (exact: ties and NaNs go to the merge, which orders by the full key).
-template <int WPR, bool VEC>
+// R: list registers per lane (k <= 64 R, WaveList of wave_topk.h)
+template <int WPR, bool VEC, int R>
 __global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict__ S, int64_t rows, int64_t cols,
                                                         int64_t ld, int k, int32_t* __restrict__ out_idx,
                                                         float* __restrict__ out_val) {
-    __shared__ uint64_t lists[4][kWave];
+    __shared__ uint64_t lists[4][R][kWave];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int sub = wave % WPR;                       // this wave's part of its row
     const int64_t row = (int64_t)blockIdx.x * (4 / WPR) + wave / WPR;
     if (row >= rows) return;                          // no barrier is reached by a missing row's waves
     const float* s = S + row * ld;
-    uint64_t top = 0;
+    WaveList<R> top;
+    top.clear();
     constexpr int V = VEC ? 4 : 1;
     const int64_t stride = (int64_t)kWave * V * WPR;  // columns per wave round
     for (int64_t base = (int64_t)sub * kWave * V; base < cols; base += stride * kUnroll) {
@@ -49,7 +51,7 @@ __global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict_
                 v[u][0] = c0 < cols ? s[c0] : 0.0f;
             }
         }
-        const uint32_t thr_hi = (uint32_t)(shfl_u64(top, k - 1) >> 32);
+        const uint32_t thr_hi = (uint32_t)(top.at(k - 1) >> 32);
         bool any = false;
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u)
@@ -61,19 +63,27 @@ __global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict_
 #pragma unroll
             for (int j = 0; j < V; ++j) {
                 const int64_t c = base + u * stride + (int64_t)lane * V + j;
-                wave_topk_push(top, c < cols ? make_key(v[u][j], (int32_t)c) : 0ull, k, lane);
+                top.push(c < cols ? make_key(v[u][j], (int32_t)c) : 0ull, k, lane);
             }
     }
     if (WPR > 1) {
-        lists[wave][lane] = top;
+#pragma unroll
+        for (int r = 0; r < R; ++r) lists[wave][r][lane] = top.t[r];
         __syncthreads();
         if (sub != 0) return;
 #pragma unroll
-        for (int w = 1; w < WPR; ++w) wave_topk_push(top, lists[wave + w][lane], k, lane);
+        for (int w = 1; w < WPR; ++w)
+#pragma unroll
+            for (int r = 0; r < R; ++r) top.push(lists[wave + w][r][lane], k, lane);
     }
-    if (lane < k) {
-        out_idx[row * k + lane] = top ? key_index(top) : -1;
-        if (out_val) out_val[row * k + lane] = top ? key_score(top) : -INFINITY;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = 64 * r + lane;
+        if (e < k) {
+            const uint64_t key = top.t[r];
+            out_idx[row * k + e] = key ? key_index(key) : -1;
+            if (out_val) out_val[row * k + e] = key ? key_score(key) : -INFINITY;
+        }
     }
 }
 
@@ -155,6 +165,21 @@ __global__ __launch_bounds__(kFoldUsers) void foldout_staged_kernel(const int32_
     for (int i = t; i < nu * W; i += kFoldUsers) results[u0 * W + i] = oimg[(i / W) * S + i % W];
 }
 
+template <int R>
+int launch_topk_rows(const float* S, int64_t rows, int64_t cols, int64_t ld, int k, int32_t* out_idx,
+                     float* out_val, bool vec, hipStream_t st) {
+    if (cols >= 16384) {
+        if (vec) topk_rows_kernel<4, true, R><<<(unsigned)rows, 256, 0, st>>>(S, rows, cols, ld, k, out_idx, out_val);
+        else topk_rows_kernel<4, false, R><<<(unsigned)rows, 256, 0, st>>>(S, rows, cols, ld, k, out_idx, out_val);
+    } else {
+        const unsigned grid = (unsigned)ceil_div(rows, 4);
+        if (vec) topk_rows_kernel<1, true, R><<<grid, 256, 0, st>>>(S, rows, cols, ld, k, out_idx, out_val);
+        else topk_rows_kernel<1, false, R><<<grid, 256, 0, st>>>(S, rows, cols, ld, k, out_idx, out_val);
+    }
+    LGX_LAUNCH_CHECK();
+    return LGX_OK;
+}
+
 }  // namespace
 }  // namespace lgx
 
@@ -164,20 +189,13 @@ extern "C" int lgx_topk_rows(const float* S, int64_t rows, int64_t cols, int64_t
                              int32_t* out_idx, float* out_val, lgx_stream_t stream) {
     LGX_REQUIRE(rows >= 0 && cols >= 0 && ld >= cols && out_idx && (rows == 0 || S), LGX_ERR_INVALID_ARG,
                 "lgx_topk_rows: bad arguments");
-    LGX_REQUIRE(k >= 1 && k <= 64, LGX_ERR_UNSUPPORTED, "lgx_topk_rows: k=%d outside [1, 64]", k);
+    LGX_REQUIRE(k >= 1 && k <= kMaxTopK, LGX_ERR_UNSUPPORTED, "lgx_topk_rows: k=%d outside [1, %d]", k, kMaxTopK);
     if (rows == 0) return LGX_OK;
     const bool vec = ld % 4 == 0 && ((uintptr_t)S & 15) == 0;
     hipStream_t st = as_hip(stream);
-    if (cols >= 16384) {
-        if (vec) topk_rows_kernel<4, true><<<(unsigned)rows, 256, 0, st>>>(S, rows, cols, ld, k, out_idx, out_val);
-        else topk_rows_kernel<4, false><<<(unsigned)rows, 256, 0, st>>>(S, rows, cols, ld, k, out_idx, out_val);
-    } else {
-        const unsigned grid = (unsigned)ceil_div(rows, 4);
-        if (vec) topk_rows_kernel<1, true><<<grid, 256, 0, st>>>(S, rows, cols, ld, k, out_idx, out_val);
-        else topk_rows_kernel<1, false><<<grid, 256, 0, st>>>(S, rows, cols, ld, k, out_idx, out_val);
-    }
-    LGX_LAUNCH_CHECK();
-    return LGX_OK;
+    if (k <= 64) return launch_topk_rows<1>(S, rows, cols, ld, k, out_idx, out_val, vec, st);
+    if (k <= 128) return launch_topk_rows<2>(S, rows, cols, ld, k, out_idx, out_val, vec, st);
+    return launch_topk_rows<4>(S, rows, cols, ld, k, out_idx, out_val, vec, st);
 }
 
 extern "C" int lgx_foldout_metrics(const int32_t* rankings, int64_t users, int k,

@@ -80,4 +80,59 @@ __device__ __forceinline__ void wave_topk_push(uint64_t& top, uint64_t cand, int
     if (lane >= k) top = 0ull;
 }
 
+// The same running list for k up to 64 R: element e = 64 r + lane lives in register r of lane
+// `lane`, sorted descending over e.  Exchanges at distances >= 64 stay inside a lane (register r
+// with r ^ (j / 64)); shorter ones are the xor-shuffles of the R = 1 network.  The reference's
+// top-k has no size limit (tools.h:13-33 partial_sort_copy, torch.topk); R = 4 covers k <= 256.
+template <int R>
+struct WaveList {
+    uint64_t t[R];  // t[r] in lane l: element 64 r + l
+
+    __device__ __forceinline__ void clear() {
+#pragma unroll
+        for (int r = 0; r < R; ++r) t[r] = 0ull;
+    }
+    __device__ __forceinline__ uint64_t at(int e) const {  // wave-uniform e
+        uint64_t v = t[0];
+#pragma unroll
+        for (int r = 1; r < R; ++r) v = (e >> 6) == r ? t[r] : v;
+        return shfl_u64(v, e & 63);
+    }
+    // bitonic merge (descending) of a bitonic sequence of 64 R elements
+    __device__ __forceinline__ void merge_desc(int lane) {
+#pragma unroll
+        for (int j = 32 * R; j >= 64; j >>= 1) {
+            const int jr = j >> 6;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (r & jr) continue;
+                const uint64_t a = t[r], b = t[r | jr];
+                t[r] = a > b ? a : b;
+                t[r | jr] = a > b ? b : a;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) t[r] = wave_merge_desc(t[r], lane);
+    }
+    // merge one batch of 64 candidates (one per lane); all 64 lanes, wave-uniform control flow
+    __device__ __forceinline__ void push(uint64_t cand, int k, int lane) {
+        if (R == 1) {
+            wave_topk_push(t[0], cand, k, lane);
+            return;
+        }
+        const uint64_t thr = at(k - 1);
+        const bool c = cand > thr;
+        if (__ballot(c) == 0ull) return;
+        cand = wave_sort_desc(c ? cand : 0ull, lane);
+        // half-cleaner of [list (desc) | candidates reversed and zero-padded (asc)]: only the last
+        // register block meets a non-zero partner; the result is bitonic over the 64 R elements
+        const uint64_t rev = shfl_u64(cand, 63 - lane);
+        t[R - 1] = t[R - 1] > rev ? t[R - 1] : rev;
+        merge_desc(lane);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (64 * r + lane >= k) t[r] = 0ull;
+    }
+};
+
 }  // namespace lgx

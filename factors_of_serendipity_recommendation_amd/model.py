@@ -171,8 +171,19 @@ class LightGCN(BasicModel):
     def bpr_loss(self, users, pos, neg):
         """model.py:196-209.  f32 tables go through the fused kernels (_BPRLoss); other dtypes
         through the reference's torch ops (bpr_loss_torch)."""
-        light = self._light_out()
         w_u, w_i = self.embedding_user.weight, self.embedding_item.weight
+        if not getattr(self, "_lgx_trusted_indices", False):
+            # the reference's torch indexing raises on a bad id; the fused kernel would turn the
+            # loss into NaN instead, so check the ranges here (one host sync).  BPR_train_original
+            # skips this for its own sampler's draws, which are in range by construction.
+            lim = torch.tensor([self.num_users, self.num_items, self.num_items], device=w_u.device)
+            idx = [t.reshape(-1).long() for t in (users, pos, neg)]
+            if idx[0].numel():
+                lo = torch.stack([t.min() for t in idx])
+                hi = torch.stack([t.max() for t in idx])
+                if bool(((lo < 0) | (hi >= lim)).any()):
+                    raise IndexError("bpr_loss: user / item index out of range")
+        light = self._light_out()
         if light.dtype == w_u.dtype == w_i.dtype == torch.float32 and light.is_contiguous():
             return _BPRLoss.apply(light, w_u, w_i, users, pos, neg)
         return self.bpr_loss_torch(users, pos, neg)

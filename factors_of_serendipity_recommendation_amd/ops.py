@@ -246,13 +246,24 @@ def foldout_metrics(rankings: torch.Tensor, truth: Tuple[torch.Tensor, torch.Ten
 
 def gather_scores(emb_user: torch.Tensor, emb_item: torch.Tensor, cand: Tuple[torch.Tensor, torch.Tensor],
                   n_pairs: int) -> torch.Tensor:
-    """Per-user candidate dots (recommend.py:167-171, :214-217) -> f32 [n_pairs]."""
+    """Per-user candidate dots (recommend.py:167-171, :214-217) -> f32 [n_pairs].  List u is scored
+    against emb_user row u, so there must be at most emb_user.shape[0] lists; a candidate id outside
+    the item table raises IndexError, as the reference's numpy indexing does."""
     require_gpu(emb_user, emb_item)
     eu = emb_user.to(torch.float32).contiguous()
     ei = emb_item.to(torch.float32).contiguous()
+    n_lists = int(cand[0].numel()) - 1
+    if n_lists < 0 or n_lists > eu.shape[0]:
+        raise ValueError(f"{n_lists} candidate lists for {eu.shape[0]} user rows")
+    if n_pairs and cand[1].numel():
+        items = cand[1][:n_pairs]
+        lo, hi = int(items.min()), int(items.max())
+        if lo < 0 or hi >= ei.shape[0]:
+            raise IndexError(f"candidate item id {lo if lo < 0 else hi} out of range for {ei.shape[0]} items")
     out = torch.empty(max(n_pairs, 1), dtype=torch.float32, device=eu.device)
-    _lib.check(_lib.lib().lgx_gather_scores(eu.data_ptr(), ei.data_ptr(), eu.shape[0], eu.shape[1], cand[0].data_ptr(),
-                                            cand[1].data_ptr(), n_pairs, out.data_ptr(), _stream_ptr(eu.device)),
+    _lib.check(_lib.lib().lgx_gather_scores(eu.data_ptr(), ei.data_ptr(), n_lists, ei.shape[0], eu.shape[1],
+                                            cand[0].data_ptr(), cand[1].data_ptr(), n_pairs, out.data_ptr(),
+                                            _stream_ptr(eu.device)),
                "lgx_gather_scores")
     return out[:n_pairs]
 

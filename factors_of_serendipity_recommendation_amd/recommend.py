@@ -42,8 +42,11 @@ def ragged_topk(scores: torch.Tensor, indptr: torch.Tensor, items: torch.Tensor,
     U = indptr.shape[0] - 1
     lens = torch.diff(indptr)
     width = int(lens.max().item()) if U else 0
-    if width < K:
-        raise ValueError(f"every user needs at least K={K} candidates")
+    shortest = int(lens.min().item()) if U else 0
+    if U and shortest < K:
+        # np.argpartition(score, -K) raises on a list shorter than K (recommend.py:53-56); never
+        # return -inf padding positions, which would index the next user's candidates
+        raise ValueError(f"every user needs at least K={K} candidates (shortest list has {shortest})")
     dense = torch.full((U, width), float("-inf"), dtype=torch.float32, device=scores.device)
     rows = torch.repeat_interleave(torch.arange(U, device=scores.device), lens)
     cols = torch.arange(scores.numel(), device=scores.device) - indptr[:-1][rows]

@@ -51,6 +51,9 @@ class Adam(torch.optim.Optimizer):
                                                     float(b1), float(b2), float(group["eps"]),
                                                     int(st["step"].item()), _stream_ptr(p.device)),
                            "lgx_adam_step")
+                # the kernel wrote p through a raw pointer: bump its version counter so that
+                # version-keyed caches (LightGCN's eval-mode propagation) see the update
+                torch.autograd.graph.increment_version(p)
         return loss
 
 
@@ -92,10 +95,15 @@ def BPR_train_original(dataset, recommend_model, loss_class: BPRLoss, epoch: int
     users, posItems, negItems = S[perm, 0], S[perm, 1], S[perm, 2]
     total_batch = len(users) // batch_size + 1
     aver_loss = torch.zeros((), device=S.device)
-    for batch_i, i in enumerate(range(0, len(users), batch_size)):  # utils.minibatch
-        cri = loss_class.stageOne(users[i:i + batch_size], posItems[i:i + batch_size], negItems[i:i + batch_size])
-        aver_loss += cri
-        if w is not None:
-            w.add_scalar("BPRLoss/BPR", float(cri), epoch * int(len(users) / batch_size) + batch_i)
+    Recmodel._lgx_trusted_indices = True  # the sampler's rows are in range by construction
+    try:
+        for batch_i, i in enumerate(range(0, len(users), batch_size)):  # utils.minibatch
+            cri = loss_class.stageOne(users[i:i + batch_size], posItems[i:i + batch_size],
+                                      negItems[i:i + batch_size])
+            aver_loss += cri
+            if w is not None:
+                w.add_scalar("BPRLoss/BPR", float(cri), epoch * int(len(users) / batch_size) + batch_i)
+    finally:
+        Recmodel._lgx_trusted_indices = False
     aver_loss = float(aver_loss) / total_batch
     return f"loss{aver_loss:.3f}-|Sample:{t_sample:.2f}|"

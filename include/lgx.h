@@ -163,14 +163,14 @@ int lgx_score_topk_workspace(int64_t B, int64_t n_items, int k, size_t* ws_bytes
  *   (may be NULL).  Masked items rank after every unmasked item with value mask_value.
  *   Ranking: higher raw score first, ties -> lower item id.  out_val = raw score, or
  *   sigmoid(score) if apply_sigmoid.  minmax_out (NULL = skip) receives {min, max} of ALL raw
- *   scores (before masking) as f32[2].  k in [1, 64].
+ *   scores (before masking) as f32[2].  k in [1, 256] (k <= 32 runs the LDS-staged bf16 kernel).
  */
 int lgx_score_topk(const void* Q, const int64_t* user_rows, const void* items, int64_t B,
                    int64_t n_items, int64_t d, int dtype, const int64_t* mask_indptr,
                    const int32_t* mask_indices, int k, float mask_value, int apply_sigmoid,
                    int32_t* out_idx, float* out_val, float* minmax_out, void* ws,
                    size_t ws_bytes, lgx_stream_t stream);
-/* Row-wise top-k of a dense f32 matrix (row stride ld), ties -> lower column.  k in [1, 64]. */
+/* Row-wise top-k of a dense f32 matrix (row stride ld), ties -> lower column.  k in [1, 256]. */
 int lgx_topk_rows(const float* S, int64_t rows, int64_t cols, int64_t ld, int k, int32_t* out_idx,
                   float* out_val, lgx_stream_t stream);
 
@@ -187,10 +187,13 @@ int lgx_foldout_metrics(const int32_t* rankings, int64_t users, int k, const int
 /* ---------------------------------------------------------------- a11/a12: candidate similarity */
 /*
  * scores[p] = <emb_user[row of p], emb_item[cand_items[p]]> for the ragged candidate lists
- * cand_indptr [U+1] int64 / cand_items int32 (f32 tables); n_pairs = cand_indptr[U] (host value).
+ * cand_indptr [n_users+1] int64 / cand_items int32 (f32 tables); n_pairs = cand_indptr[n_users]
+ * (host value).  n_users = number of candidate lists: emb_user must hold at least that many rows.
+ * n_items = rows of emb_item; a candidate id outside [0, n_items) is never read and scores NaN
+ * (the Python layer raises IndexError before the launch, as numpy indexing would).
  */
-int lgx_gather_scores(const float* emb_user, const float* emb_item, int64_t n_users, int64_t d,
-                      const int64_t* cand_indptr, const int32_t* cand_items, int64_t n_pairs,
+int lgx_gather_scores(const float* emb_user, const float* emb_item, int64_t n_users, int64_t n_items,
+                      int64_t d, const int64_t* cand_indptr, const int32_t* cand_items, int64_t n_pairs,
                       float* scores, lgx_stream_t stream);
 
 /* ---------------------------------------------------------------- 8(f) rank 4: stratified candidates */
@@ -210,6 +213,12 @@ int lgx_strat_labels(const float* scores, int64_t n_users, int64_t n_items, floa
 int lgx_strat_select(const int8_t* labels, int64_t n_users, int64_t n_items, const int32_t* hist, int n_bins,
                      const int32_t* targets, uint64_t seed, int32_t* out, int out_stride, int32_t* out_count,
                      lgx_stream_t stream);
+/* the same with flags: LGX_STRAT_EXACT runs the radix select for every row (the fast path's
+ * cut-and-rank must pick identical sets; used by the parity tests) */
+#define LGX_STRAT_EXACT 1
+int lgx_strat_select_ex(const int8_t* labels, int64_t n_users, int64_t n_items, const int32_t* hist, int n_bins,
+                        const int32_t* targets, uint64_t seed, int32_t* out, int out_stride, int32_t* out_count,
+                        int flags, lgx_stream_t stream);
 
 /* ---------------------------------------------------------------- 8(f) rank 3: interaction files */
 /*

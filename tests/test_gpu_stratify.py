@@ -37,14 +37,15 @@ def _labels(eu, ei, train, num_fold=10):
     return lab, hist, min16, inter16
 
 
-def _select(lab, hist, targets, seed, n_bins=11, stride=None):
+def _select(lab, hist, targets, seed, n_bins=11, stride=None, flags=0):
     U, I = lab.shape
     stride = stride or int(max(targets))
     out = torch.empty((U, stride), dtype=torch.int32, device=DEV)
     cnt = torch.empty(U, dtype=torch.int32, device=DEV)
     tgt = torch.as_tensor(np.asarray(targets, dtype=np.int32), device=DEV)
-    _lib.check(_lib.lib().lgx_strat_select(lab.data_ptr(), U, I, hist.data_ptr(), n_bins, tgt.data_ptr(), seed,
-                                           out.data_ptr(), stride, cnt.data_ptr(), None), "lgx_strat_select")
+    _lib.check(_lib.lib().lgx_strat_select_ex(lab.data_ptr(), U, I, hist.data_ptr(), n_bins, tgt.data_ptr(), seed,
+                                              out.data_ptr(), stride, cnt.data_ptr(), flags, None),
+               "lgx_strat_select_ex")
     return out.cpu().numpy(), cnt.cpu().numpy()
 
 
@@ -120,7 +121,7 @@ def test_create_candidates_stratification_dropin(tmp_path):
     assert os.path.exists(root / "s" / "rec" / "3" / "candidate.npy")
 
 
-def test_fast_select_equals_radix_select(monkeypatch):
+def test_fast_select_equals_radix_select():
     """the cut-and-rank fast path picks exactly the sets (and order) of the exact radix select:
     long rows (fast path taken), a tiny label (cut = everything), and a row whose candidates
     overflow the fast path's buffer (falls back inside the same launch)"""
@@ -137,8 +138,7 @@ def test_fast_select_equals_radix_select(monkeypatch):
     hist = torch.from_numpy(hist_h).to(DEV)
     targets = [1000, 1000, 900, 37, 1024, 1]
     fast = _select(lab, hist, targets, seed=12345, stride=1024)
-    monkeypatch.setenv("LGX_STRAT_EXACT", "1")
-    exact = _select(lab, hist, targets, seed=12345, stride=1024)
+    exact = _select(lab, hist, targets, seed=12345, stride=1024, flags=_lib.LGX_STRAT_EXACT)
     assert np.array_equal(fast[1], exact[1])
     for u in range(U):
         assert np.array_equal(fast[0][u, :fast[1][u]], exact[0][u, :exact[1][u]])
