@@ -1,25 +1,39 @@
 """Benchmark of the LightGCN hot path on MI355X (contract: one JSON line from rank 0).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config synth10m] [--score-users 65536]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config synth10m] [--score-users 1000000]
   N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 Workload (BASELINE.json): the propagation metric is quoted at 1/2/4/8 GPUs on configs[3]
 ("Synthetic 10M users x 1M items, 500M edges, K=3, d=128, row-sharded with RCCL all-gather"),
 which fits one MI355X (CSR 8 GB + tables < 30 GB of 288 GB), so it is the N=1 workload too and the
 total graph is fixed as N grows (strong scaling).  One step = one full K-layer propagation
-(LightGCN.computer(), model.py:145-177) with bf16 embedding storage and fp32 accumulation.
-The scoring metric (configs[4]: user x item MFMA scoring + train mask + top-20, d=256 bf16, 1M
-items) is reported in the same line under "scoring": one step scores a fixed batch of query users
-against the full catalog, the batch split across ranks.
+(LightGCN.computer(), model.py:145-177).  `value` is the bf16-storage / fp32-accumulate run (SURVEY
+C4: "fp32 parity; bf16 perf"); the same line carries the fp32-storage run (the north-star
+precision) under "fp32".  The scoring metric (configs[4]: user x item MFMA scoring + train mask +
+top-20, d=256 bf16, 1M items) is reported under "scoring": one step scores a fixed batch of query
+users against the full catalog, the batch split across ranks.
 
 value = K * nnz(A^) * steps / t  (edges/s), t = max over ranks of the barrier-bracketed loop.
-roofline.achieved = algorithmic bytes per SpMM launch / mean launch time (HIP events on the
-compute stream), bytes per layer = nnz*(4 + 4 + d*s) + rows*d*s + 8*(rows+1).
+
+SpMM roofline (per launch of spmm_segments + spmm_fixup, HIP events on the compute stream):
+  * achieved = model bytes / mean launch time, where the model is cache-aware: the CSR stream
+    (8 B/nnz + indptr), the layer's epilogue I/O (mode-dependent), and every gathered table row
+    EXCEPT those of the hottest rows that fit one XCD's 4 MiB L2 (by column degree, per table).
+    Those rows are served from L2 at 19.4 TB/s (profiles/r02_fetch_calibration.json sweep), so a
+    schedule cannot be made to pull them from HBM; every other gather is counted as one HBM row
+    read.  This stays below the kernel's measured L2-miss traffic, so frac <= 1.
+  * floor_bytes = nnz*8 + 2*N*d*s (SURVEY 8(d) compulsory floor); gathered_bytes = every gathered
+    row counted (the SURVEY 8(d) figure, which can exceed the HBM peak on cached rows).
+  * traffic = calibrated rocprofv3 counter bytes per launch (2 x FETCH_SIZE + WRITE_SIZE; the x2
+    measured for this access pattern in profiles/r02_fetch_calibration.json) from this round's PMC
+    profile, used only when that profile was taken from the same liblgx.so build (sha256).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
+import math
 import os
 import sys
 import time
@@ -38,7 +52,9 @@ from factors_of_serendipity_recommendation_amd.synth import CONFIGS, synth_graph
 
 HBM_PEAK = 8.0e12        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BF16_MFMA_PEAK = 2.5e15  # dense bf16 MFMA spec
+L2_BYTES = 4 << 20       # per XCD
 METRIC = "LightGCN prop edges/s + full-catalog score items/s at 1/2/4/8 MI355X"
+CALIB = "profiles/r02_fetch_calibration.json"
 
 
 def log(*a):
@@ -61,46 +77,83 @@ def max_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
-def measured_traffic(config: str, world: int, kernels) -> tuple:
-    """HBM bytes per launch from the newest committed rocprofv3 PMC summary for this workload
-    (profiles/rNN_<config>_pmc_traffic.json; (2*FETCH_SIZE + WRITE_SIZE) per MI355X_MICROARCH.md).
-    Returns (GB per launch or None, source file)."""
+def lib_sha() -> str:
+    h = hashlib.sha256()
+    with open(_lib.LIB_PATH, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()[:16]
+
+
+def measured_traffic(config: str, dtype: str, world: int, kernels) -> tuple:
+    """Calibrated counter bytes per launch from the newest committed PMC summary of this workload
+    (profiles/rNN_<config>_pmc_traffic.json), if it was collected from the library build that is
+    running now.  Returns (GB per launch or None, source or reason)."""
     import glob
     if world != 1:
-        return None, None
+        return None, "PMC profiles are single-GPU"
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_pmc_traffic.json")))
     if not files:
-        return None, None
+        return None, "no PMC profile"
     doc = json.load(open(files[-1]))
+    src = os.path.relpath(files[-1], ROOT)
+    if doc.get("lib_sha256_16") != lib_sha():
+        return None, f"{src} was taken from another liblgx.so build"
     try:
-        b = sum(doc["kernels"][k]["hbm_bytes_per_launch"] for k in kernels)
+        b = sum(doc["kernels"][dtype][k]["hbm_bytes_per_launch"] for k in kernels)
     except KeyError:
-        return None, None
-    return b / 1e9, os.path.relpath(files[-1], ROOT)
+        return None, f"{src} has no {dtype} entry"
+    return b / 1e9, src
 
 
-def layer_bytes(nnz: int, rows: int, d: int, s: int, out_s: int = 0) -> int:
-    """col id + value + one gathered row per nonzero, one output row per row, indptr."""
-    return nnz * (4 + 4 + d * s) + rows * d * (out_s or s) + 8 * (rows + 1)
+def epilogue_bytes(mode: int, rows: int, d: int, s: int) -> int:
+    """Bytes the layer epilogue moves per mode (ops.propagate_layer modes, spmm.hip finish_chunk)."""
+    t, f = rows * d * s, rows * d * 4
+    return {_lib.LGX_LAYER_PLAIN: t, _lib.LGX_LAYER_FIRST: t + t + f, _lib.LGX_LAYER_MID: t + 2 * f,
+            _lib.LGX_LAYER_LAST: 2 * f, _lib.LGX_LAYER_ONLY: t + f, _lib.LGX_LAYER_PARTIAL: f}[mode]
 
 
-def bench_propagation(args, rank, world):
-    cfg = CONFIGS[args.config]
-    dtype = torch.bfloat16 if (args.dtype or cfg.dtype) == "bf16" else torch.float32
+def cold_gather_rows(A, d: int, s: int) -> tuple:
+    """Gathers per layer of rows outside each table's L2-resident hot set: (cold nnz, hot rows,
+    hot fraction).  Column degree == row degree (A^ symmetric); the user rows gather the item table
+    and the item rows the user table, each its own hot set."""
+    deg = torch.diff(A.indptr)
+    R = max(1, L2_BYTES // (d * s))
+    U, I = A.n_users, A.n_items
+    tables = [deg[:U], deg[U:]] if U > 0 and I > 0 else [deg]
+    total = int(deg.sum())
+    hot = sum(int(torch.topk(t, min(R, t.numel())).values.sum()) for t in tables if t.numel())
+    return total - hot, R, hot / max(1, total)
+
+
+def layer_models(A, d: int, s: int, mode: int) -> dict:
+    nnz, rows, N = A.nnz, A.n_rows, A.n_cols
+    csr = nnz * 8 + 8 * (rows + 1)
+    epi = epilogue_bytes(mode, rows, d, s)
+    cold, R, hot_frac = cold_gather_rows(A, d, s)
+    return {"model": csr + epi + cold * d * s, "gathered": csr + epi + nnz * d * s,
+            "floor": nnz * 8 + 2 * N * d * s, "hot_rows": R, "hot_frac": hot_frac}
+
+
+def calibration() -> dict:
+    path = os.path.join(ROOT, CALIB)
+    if not os.path.exists(path):
+        return {}
+    doc = json.load(open(path))
+    c = doc["cases"]
+    return {"source": CALIB, "fetch_size_factor_random_256B_rows": round(c["once_256"]["known_over_fetch_size"], 3),
+            "fetch_size_counts_mall_hits": c["hot_mall"]["known_over_fetch_size"] < 3.0,
+            "gather_rate_by_table_size_tbs": doc.get("sweep_256", {})}
+
+
+def make_step(A, E0, K, d, dtype, world, cfg, rank, timings):
     es = 2 if dtype == torch.bfloat16 else 4
-    t0 = time.time()
-    A = synth_graph(cfg, seed=2020, device="cuda")
-    N = cfg.n_users + cfg.n_items
-    log(f"[bench] graph {cfg.name}: N={N} nnz={A.nnz} built in {time.time() - t0:.1f}s")
-    E0 = lgx.fill_normal((N, cfg.d), 0.1, 2020, dtype=dtype)
-    K, d = cfg.K, cfg.d
-    timings = []  # (start, end) events around every SpMM layer launch on the compute stream
-
+    N = A.n_rows if world == 1 else None
     if world == 1:
         out = torch.empty((N, d), dtype=torch.float32, device="cuda")
         bufs = [torch.empty((N, d), dtype=dtype, device="cuda") for _ in range(2)]
         acc = torch.empty((N, d), dtype=torch.float32, device="cuda")
-        local_nnz, local_rows = A.nnz, N
+        models = {}
 
         def step(record):
             X = E0
@@ -114,92 +167,140 @@ def bench_propagation(args, rank, world):
                 ops.propagate_layer(A, X, mode, Y=Y, E0=E0, acc=acc, out=out, n_mean=float(K + 1))
                 if record:
                     e1.record()
-                    timings.append((e0, e1, layer_bytes(A.nnz, A.n_rows, d, es)))
+                    if mode not in models:
+                        models[mode] = layer_models(A, d, es, mode)
+                    timings.append((e0, e1, models[mode]))
                 X = Y
-    else:
-        shard = make_shard(A, cfg.n_users, cfg.n_items, rank, world)
-        del A
-        torch.cuda.empty_cache()
-        prop = ShardedPropagation(shard, E0[:cfg.n_users], E0[cfg.n_users:], K)
-        del E0
-        local_nnz = shard.A_pull.nnz + shard.A_push.nnz  # every edge of the rank's users, both directions
-        local_rows = shard.n_u_local + shard.n_i_local
+        return step, A.nnz, A.n_rows
+    shard = make_shard(A, cfg.n_users, cfg.n_items, rank, world)
+    prop = ShardedPropagation(shard, E0[:cfg.n_users], E0[cfg.n_users:], K)
+    models = {}
 
-        def layer_fn(Aop, X, mode, **kw):
-            if step.record:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-            ops.propagate_layer(Aop, X, mode, **kw)
-            if step.record:
-                e1.record()
-                # the push launch writes fp32 partial sums
-                out_s = 4 if mode == _lib.LGX_LAYER_PARTIAL else es
-                timings.append((e0, e1, layer_bytes(Aop.nnz, Aop.n_rows, d, es, out_s)))
+    def layer_fn(Aop, X, mode, **kw):
+        if step.record:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        ops.propagate_layer(Aop, X, mode, **kw)
+        if step.record:
+            e1.record()
+            nnz, rows = Aop.nnz, Aop.n_rows
+            key = (id(Aop), mode)
+            if key not in models:
+                epi = epilogue_bytes(mode, rows, d, es)
+                csr = nnz * 8 + 8 * (rows + 1)
+                models[key] = {"model": csr + epi + nnz * d * es, "gathered": csr + epi + nnz * d * es,
+                               "floor": nnz * 8 + rows * d * es + Aop.n_cols * d * es, "hot_rows": 0, "hot_frac": 0.0}
+            timings.append((e0, e1, models[key]))
 
-        prop.layer_fn = layer_fn
+    prop.layer_fn = layer_fn
 
-        def step(record):
-            step.record = record
-            prop.step()
-        step.record = False
+    def step(record):
+        step.record = record
+        prop.step()
+    step.record = False
+    return step, shard.A_pull.nnz + shard.A_push.nnz, shard.n_u_local + shard.n_i_local
 
+
+def bench_propagation(args, rank, world, A, cfg, dtype, steps, warmup):
+    es = 2 if dtype == torch.bfloat16 else 4
+    dname = "bf16" if es == 2 else "f32"
+    K, d = cfg.K, cfg.d
+    N = cfg.n_users + cfg.n_items
+    E0 = lgx.fill_normal((N, d), 0.1, 2020, dtype=dtype)
+    timings = []
+    step, local_nnz, _ = make_step(A, E0, K, d, dtype, world, cfg, rank, timings)
     nnz_all = local_nnz
     if world > 1:
         t = torch.tensor([local_nnz], dtype=torch.int64, device="cuda")
         dist.all_reduce(t)
         nnz_all = int(t.item())
-
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step(False)
     barrier_sync(world)
     t_start = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step(True)
     barrier_sync(world)
     elapsed = max_over_ranks(time.perf_counter() - t_start, world)
-    # per-launch time of the dominant kernel family (spmm_segments + its fix-up pass)
-    launch_ms = [e0.elapsed_time(e1) for e0, e1, _ in timings]
-    mean_launch_s = float(np.mean(launch_ms)) / 1e3
-    bytes_per_launch = float(np.mean([b for _, _, b in timings]))
-    achieved = bytes_per_launch / mean_launch_s
-    edges = K * nnz_all * args.steps
-    traffic, traffic_src = measured_traffic(cfg.name, world, ["spmm_segments", "spmm_fixup"])
-    res = {
-        "cfg": cfg, "dtype": "bf16" if es == 2 else "f32", "value": edges / elapsed,
-        "ms_per_step": elapsed / args.steps * 1e3, "nnz": nnz_all,
-        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK, "traffic": traffic, "traffic_unit": "GB/launch",
-                     "traffic_source": traffic_src,
-                     "kernel": "spmm_segments (+spmm_fixup)", "bytes_per_launch": int(bytes_per_launch),
-                     "mean_launch_ms": mean_launch_s * 1e3,
-                     # achieved counts every gathered row as an HBM read, so the caches that serve part
-                     # of them can lift frac above 1; the PMC bytes over the same launch time are the
-                     # HBM rate the kernel really pulls
-                     "traffic_rate_gbs": traffic / mean_launch_s if traffic else None,
-                     "traffic_frac": traffic * 1e9 / mean_launch_s / HBM_PEAK if traffic else None},
-        "graph": A if world == 1 else None, "E0": E0 if world == 1 else None,
-    }
-    return res
+    launch_s = np.array([e0.elapsed_time(e1) for e0, e1, _ in timings]) / 1e3
+    mean_launch_s = float(launch_s.mean())
+    mean = {key: float(np.mean([m[key] for _, _, m in timings])) for key in ("model", "gathered", "floor")}
+    hot_rows, hot_frac = timings[0][2]["hot_rows"], timings[0][2]["hot_frac"]
+    traffic, tsrc = measured_traffic(cfg.name, dname, world, ["spmm_segments", "spmm_fixup"])
+    achieved = mean["model"] / mean_launch_s
+    roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK, "traffic": traffic,
+            "kernel": "spmm_segments (+spmm_fixup): " + ops.spmm_kernel_name(d, dtype, A.plan.seg_len if world == 1
+                                                                             else 8192),
+            "mean_launch_ms": mean_launch_s * 1e3,
+            "bytes_model": "cache-aware: CSR + epilogue + gathers of rows outside the per-XCD L2 hot set "
+                           f"(top {hot_rows} rows per table by degree = {hot_frac:.3f} of gathers)"
+                           if world == 1 else "per-rank operators, every gather counted",
+            "bytes_per_launch": int(mean["model"]),
+            "floor_bytes_per_launch": int(mean["floor"]), "floor_rate_gbs": mean["floor"] / mean_launch_s / 1e9,
+            "floor_frac": mean["floor"] / mean_launch_s / HBM_PEAK,
+            "gathered_bytes_per_launch": int(mean["gathered"]),
+            "gathered_rate_gbs": mean["gathered"] / mean_launch_s / 1e9,
+            "traffic_unit": "GB/launch", "traffic_source": tsrc,
+            "traffic_rate_gbs": traffic / mean_launch_s if traffic else None,
+            "traffic_frac": traffic * 1e9 / mean_launch_s / HBM_PEAK if traffic else None}
+    if world == 1:
+        roof["calibration"] = calibration()
+    return {"dtype": dname, "value": K * nnz_all * steps / elapsed, "unit": "edges/s",
+            "ms_per_step": elapsed / steps * 1e3, "steps": steps, "warmup": warmup, "nnz": nnz_all,
+            "roofline": roof, "E0": E0 if world == 1 else None}
 
 
-def cpu_baseline(res, args):
-    """oracle/torch_ref.py (torch.sparse.mm on the host, model.py:163-175) on a bounded row block
-    of the same graph against the full fp32 table."""
+# ------------------------------------------------------------------------------------ CPU baseline
+def host_cpus() -> tuple:
+    """CPUs this process may run on: the affinity set, capped by a cgroup-v2 CPU quota if any."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    if quota is not None:
+        n = max(1, min(n, int(math.ceil(quota))))
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return n, model, quota
+
+
+def cpu_baseline(A, E0, cfg, target_nnz):
+    """oracle/torch_ref.py (torch.sparse.mm on the host, model.py:163-175) on a bounded sample of
+    BOTH row kinds of the same graph -- the first user rows (gathering the item table) and the first
+    item rows (gathering the user table) -- against the full fp32 table; rate extrapolated per edge."""
     from oracle import torch_ref
-    A, E0 = res["graph"], res["E0"]
-    cfg = res["cfg"]
-    threads = min(os.cpu_count() or 1, 16)
+    threads, model, quota = host_cpus()
     ip = A.indptr.cpu().numpy()
-    target = args.cpu_nnz
-    r1 = int(np.searchsorted(ip, target))
-    r1 = max(1, min(r1, A.n_rows))
-    nnz = int(ip[r1])
-    G = torch_ref.coo_from_csr(ip[:r1 + 1], A.indices[:nnz].cpu().numpy(), A.vals[:nnz].cpu().numpy(), A.n_cols)
     X = E0.float().cpu()
-    r = torch_ref.time_spmm_rows(G, X, cfg.K, threads)
-    return {"value": r["edges_per_s"], "unit": "edges/s", "cores": threads, "kind": "port",
-            "sample": f"rows [0,{r1}) of the same graph ({nnz} nnz, {cfg.K} x torch.sparse.mm against the full "
-                      f"fp32 [{A.n_cols},{cfg.d}] table, {r['seconds']:.1f}s)"}
+    U = cfg.n_users
+    secs, edges, parts = 0.0, 0, []
+    for name, r0 in (("user", 0), ("item", U)):
+        base = int(ip[r0])
+        r1 = int(np.searchsorted(ip, base + target_nnz // 2))
+        r1 = max(r0 + 1, min(r1, A.n_rows))
+        s, e = int(ip[r0]), int(ip[r1])
+        G = torch_ref.coo_from_csr(ip[r0:r1 + 1] - s, A.indices[s:e].cpu().numpy(), A.vals[s:e].cpu().numpy(),
+                                   A.n_cols)
+        r = torch_ref.time_spmm_rows(G, X, cfg.K, threads)
+        secs += r["seconds"]
+        edges += r["edges"]
+        parts.append(f"{name} rows [{r0},{r1}) ({e - s} nnz)")
+        del G
+    return {"value": edges / secs, "unit": "edges/s", "cores": threads, "kind": "port", "extrapolated": True,
+            "cpu_model": model, "os_cpu_count": os.cpu_count(), "cgroup_cpu_quota": quota,
+            "sample": f"{cfg.K} x torch.sparse.mm of " + " + ".join(parts) + f" against the full fp32 "
+                      f"[{A.n_cols},{cfg.d}] table, {secs:.1f}s; per-edge rate extrapolated to the whole graph"}
 
 
 def bench_scoring(args, rank, world):
@@ -230,15 +331,16 @@ def bench_scoring(args, rank, world):
     elapsed = max_over_ranks(time.perf_counter() - t_start, world)
     mean_launch = float(np.mean([a.elapsed_time(b) for a, b in ev])) / 1e3
     flops = 2.0 * B * n_items * d
-    traffic, traffic_src = measured_traffic(args.config, world, ["score_topk_bf16_lds"])
+    traffic, tsrc = measured_traffic(args.config, "scoring", world, ["score_topk_bf16_lds"])
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = scoring_cpu_baseline(Q, items, pos, k, args.cpu_score_users)
     return {"value": B_total * n_items * steps / elapsed, "unit": "items/s", "users_per_step": B_total,
             "n_items": n_items, "d": d, "k": k, "dtype": "bf16", "ms_per_step": elapsed / steps * 1e3,
+            "plan": ops.score_topk_plan(B, n_items, d, torch.bfloat16, k),
             "roofline": {"bound": "mfma", "achieved": flops / mean_launch / 1e12, "peak": BF16_MFMA_PEAK / 1e12,
                          "unit": "TFLOP/s", "frac": flops / mean_launch / BF16_MFMA_PEAK, "traffic": traffic,
-                         "traffic_unit": "GB/launch", "traffic_source": traffic_src,
+                         "traffic_unit": "GB/launch", "traffic_source": tsrc,
                          "kernel": "score_topk_bf16_lds (+ score_topk_finalize, both inside the timed launch)"},
             "cpu_baseline": cpu}
 
@@ -247,7 +349,7 @@ def scoring_cpu_baseline(Q, items, pos, k, n_users):
     """The reference's CPU scoring procedure (Procedure.py:121-135 per 100-user batch: fp32 matmul,
     sigmoid, train mask, torch.topk) on the first n_users query users of the same batch."""
     from oracle import torch_ref
-    threads = min(16, os.cpu_count() or 1)
+    threads, model, _ = host_cpus()
     torch.set_num_threads(threads)
     Qc = Q[:n_users].float().cpu()
     Ic = items.float().cpu()
@@ -255,8 +357,9 @@ def scoring_cpu_baseline(Q, items, pos, k, n_users):
     torch_ref.score_topk_cpu(Qc[:100], Ic, k, masks[:100])  # warm-up
     _, t = torch_ref.score_topk_cpu(Qc, Ic, k, masks)
     return {"value": n_users * items.shape[0] / t, "unit": "items/s", "cores": threads, "kind": "port",
+            "extrapolated": True, "cpu_model": model,
             "sample": f"{n_users} of the query users x {items.shape[0]} items, d={items.shape[1]} fp32, "
-                      f"top-{k} with the same train masks ({t:.1f}s)"}
+                      f"top-{k} with the same train masks ({t:.1f}s); per-item rate extrapolated"}
 
 
 def main():
@@ -271,6 +374,8 @@ def main():
     ap.add_argument("--score-steps", type=int, default=2)
     ap.add_argument("--cpu-nnz", type=int, default=40_000_000)
     ap.add_argument("--cpu-score-users", type=int, default=4000)
+    ap.add_argument("--fp32-steps", type=int, default=5, help="timed steps of the fp32-storage run")
+    ap.add_argument("--no-fp32", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scoring", action="store_true")
     ap.add_argument("--no-propagation", action="store_true", help="development: scoring leg only")
@@ -289,6 +394,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
             dist.init_process_group(backend)
+        log(f"[bench] world {dist.get_world_size()} over {dist.get_backend()}")
     if world != args.gpus:
         log(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}")
 
@@ -297,15 +403,26 @@ def main():
         if rank == 0:
             print(json.dumps({"metric": METRIC, "scoring": sc}), flush=True)
         return
-    res = bench_propagation(args, rank, world)
+    cfg = CONFIGS[args.config]
+    main_dtype = torch.bfloat16 if (args.dtype or cfg.dtype) == "bf16" else torch.float32
+    t0 = time.time()
+    A = synth_graph(cfg, seed=2020, device="cuda")
+    log(f"[bench] graph {cfg.name}: N={cfg.n_users + cfg.n_items} nnz={A.nnz} built in {time.time() - t0:.1f}s")
+    res = bench_propagation(args, rank, world, A, cfg, main_dtype, args.steps, args.warmup)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(res, args)
-    res.pop("graph", None)
+        cpu = cpu_baseline(A, res["E0"], cfg, args.cpu_nnz)
     res.pop("E0", None)
     torch.cuda.empty_cache()
+    fp32 = None
+    if main_dtype == torch.bfloat16 and not args.no_fp32:
+        fp32 = bench_propagation(args, rank, world, A, cfg, torch.float32, max(1, args.fp32_steps),
+                                 max(1, min(2, args.warmup)))
+        fp32.pop("E0", None)
+        fp32["note"] = "fp32 embedding storage (the north-star precision), same graph and kernel family"
+    del A
+    torch.cuda.empty_cache()
     scoring = None if args.no_scoring else bench_scoring(args, rank, world)
-    cfg = res["cfg"]
     line = {
         "metric": METRIC, "value": res["value"], "unit": "edges/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": res["ms_per_step"], "higher_is_better": True, "scaling": "strong",
@@ -313,7 +430,7 @@ def main():
         "config": {"workload": f"{cfg.name}: {cfg.n_users} users x {cfg.n_items} items, {cfg.n_edges} edges "
                                f"(nnz {res['nnz']}), K={cfg.K}, d={cfg.d}, {res['dtype']} storage / fp32 accumulate",
                    "parallelism": f"row-shard{world}" if world > 1 else "single"},
-        "roofline": res["roofline"], "cpu_baseline": cpu, "scoring": scoring,
+        "roofline": res["roofline"], "cpu_baseline": cpu, "fp32": fp32, "scoring": scoring,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)

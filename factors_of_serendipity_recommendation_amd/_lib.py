@@ -57,6 +57,8 @@ SIGNATURES = {
     "lgx_spmm_csr": (_c_int, [ctypes.POINTER(LgxCSR), _vp, _vp, _c_i64, _c_int, _vp]),
     "lgx_strat_labels": (_c_int, [_vp, _c_i64, _c_i64, _c_float, _c_float, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "lgx_strat_select": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_int, _vp, ctypes.c_uint64, _vp, _c_int, _vp, _vp]),
+    "lgx_spmm_kernel_name": (_c_int, [_c_i64, _c_int, _c_i64, ctypes.c_char_p, ctypes.c_size_t]),
+    "lgx_score_topk_plan": (_c_int, [_c_i64, _c_i64, _c_i64, _c_int, _c_int, ctypes.c_char_p, ctypes.c_size_t]),
     "lgx_strat_select_ex": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_int, _vp, ctypes.c_uint64, _vp, _c_int, _vp,
                                      _c_int, _vp]),
     "lgx_parse_lines_workspace": (_c_int, [_c_i64, _sz_p]),

@@ -1334,6 +1334,26 @@ extern "C" int lgx_score_topk_workspace(int64_t B, int64_t n_items, int k, size_
     return LGX_OK;
 }
 
+extern "C" int lgx_score_topk_plan(int64_t B, int64_t n_items, int64_t d, int dtype, int k, char* buf, size_t len) {
+    LGX_REQUIRE(buf && len > 0 && B > 0 && n_items > 0 && k >= 1 && k <= kMaxTopK, LGX_ERR_INVALID_ARG,
+                "lgx_score_topk_plan: bad arguments");
+    LGX_REQUIRE(dtype == LGX_DTYPE_F32 || dtype == LGX_DTYPE_BF16, LGX_ERR_INVALID_ARG, "lgx_score_topk_plan: dtype");
+    UserRange r[2];
+    const int n = plan_ranges(B, n_items, dtype, d, k, r);
+    size_t off = 0;
+    for (int i = 0; i < n && off < len; ++i) {
+        const SplitPlan& p = r[i].p;
+        const char* kern = p.lds ? "score_topk_bf16_lds<8 waves, 64-item tiles, 16x16x32>"
+                                 : (v1_waves(k) == 4 ? "score_topk_kernel<4 waves>" : "score_topk_kernel<1 wave>");
+        const char* mode = p.lds ? (p.n_splits == 1 ? "full-sweep" : (p.xcd_affine ? "split-xcd" : "split"))
+                                 : "split";
+        off += snprintf(buf + off, len - off, "%s%s users[%lld,%lld) %s n_splits=%d utiles=%lld",
+                        i ? "; " : "", kern, (long long)r[i].u0, (long long)r[i].u1, mode, p.n_splits,
+                        (long long)p.n_utiles);
+    }
+    return LGX_OK;
+}
+
 extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const void* items, int64_t B,
                               int64_t n_items, int64_t d, int dtype, const int64_t* mask_indptr,
                               const int32_t* mask_indices, int k, float mask_value, int apply_sigmoid,

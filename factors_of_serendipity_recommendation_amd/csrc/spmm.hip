@@ -350,6 +350,26 @@ int dispatch_layer(const LayerArgs& a, hipStream_t stream) {
     return launch_layer<T, 64, 4>(a, stream);
 }
 
+// the instantiation dispatch_layer launches, as text (lgx_spmm_kernel_name): kept next to it so
+// that the two cannot drift apart
+template <typename T>
+int dispatch_name(int64_t d, int64_t seg_len, char* buf, size_t len) {
+    constexpr int VEC = Vec<T>::N;
+    const int64_t chunks = d / VEC;
+    int G, CPL, U;
+    if (chunks <= 4) G = 4, CPL = 1;
+    else if (chunks <= 8) G = 8, CPL = 1;
+    else if (chunks <= 16) G = 16, CPL = 1;
+    else if (chunks <= 32) G = 32, CPL = 1;
+    else if (chunks <= 64) G = 64, CPL = 1;
+    else if (chunks <= 128) G = 64, CPL = 2;
+    else G = 64, CPL = 4;
+    U = CPL == 1 ? (G == 16 ? 16 : 8) : (CPL == 2 ? 4 : 2);
+    if (G == 16 && CPL == 1 && seg_len <= 128) U = 8;
+    snprintf(buf, len, "spmm_segments<%s,%d,%d,%d>", sizeof(T) == 4 ? "f32" : "bf16", G, CPL, U);
+    return LGX_OK;
+}
+
 template <typename T>
 __global__ void to_f32_scaled(const T* __restrict__ src, float* __restrict__ dst, int64_t n) {
     int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -452,6 +472,13 @@ extern "C" int lgx_layer_epilogue(const float* y, int64_t rows, void* Y, const v
     else layer_epilogue_kernel<uint16_t><<<grid, kThreads, 0, as_hip(stream)>>>(a, y, rows);
     LGX_LAUNCH_CHECK();
     return LGX_OK;
+}
+
+extern "C" int lgx_spmm_kernel_name(int64_t d, int dtype, int64_t seg_len, char* buf, size_t len) {
+    LGX_REQUIRE(buf && len > 0 && d > 0 && seg_len > 0, LGX_ERR_INVALID_ARG, "lgx_spmm_kernel_name: bad arguments");
+    LGX_REQUIRE(dtype == LGX_DTYPE_F32 || dtype == LGX_DTYPE_BF16, LGX_ERR_INVALID_ARG, "lgx_spmm_kernel_name: dtype");
+    return dtype == LGX_DTYPE_F32 ? dispatch_name<float>(d, seg_len, buf, len)
+                                  : dispatch_name<uint16_t>(d, seg_len, buf, len);
 }
 
 extern "C" int lgx_spmm_csr(const lgx_csr* A, const void* X, void* Y, int64_t d, int dtype,

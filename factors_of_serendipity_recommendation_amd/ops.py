@@ -327,3 +327,22 @@ def bpr_loss_backward(light, ego_user, ego_item, users, pos, neg, coef, grad_los
                                                 gl.data_ptr(), gr.data_ptr(), g_light.data_ptr(), g_user.data_ptr(),
                                                 g_item.data_ptr(), _stream_ptr(light.device)), "lgx_bpr_loss_backward")
     return g_light, g_user, g_item
+
+
+# ------------------------------------------------------------------------------------ introspection
+def spmm_kernel_name(d: int, dtype: torch.dtype, seg_len: int) -> str:
+    """The SpMM instantiation lgx_propagate_layer launches for this embedding dim / storage dtype /
+    plan segment length (``lgx_spmm_kernel_name``; host only)."""
+    buf = ctypes.create_string_buffer(256)
+    code = _lib.LGX_DTYPE_BF16 if dtype == torch.bfloat16 else _lib.LGX_DTYPE_F32
+    _lib.check(_lib.lib().lgx_spmm_kernel_name(int(d), code, int(seg_len), buf, 256), "lgx_spmm_kernel_name")
+    return buf.value.decode()
+
+
+def score_topk_plan(B: int, n_items: int, d: int, dtype: torch.dtype, k: int) -> str:
+    """The launch plan of lgx_score_topk for this shape (``lgx_score_topk_plan``; host only)."""
+    buf = ctypes.create_string_buffer(1024)
+    code = _lib.LGX_DTYPE_BF16 if dtype == torch.bfloat16 else _lib.LGX_DTYPE_F32
+    _lib.check(_lib.lib().lgx_score_topk_plan(int(B), int(n_items), int(d), code, int(k), buf, 1024),
+               "lgx_score_topk_plan")
+    return buf.value.decode()

@@ -140,6 +140,12 @@ int lgx_propagate_layer(const lgx_csr* A, const void* X, void* Y, const void* E0
  */
 int lgx_layer_epilogue(const float* y, int64_t rows, void* Y, const void* E0, float* acc, float* out,
                        int64_t d, int dtype, int mode, float n_mean, lgx_stream_t stream);
+/*
+ * Host-only introspection: the name of the SpMM kernel instantiation lgx_propagate_layer launches
+ * for (d, dtype, plan seg_len), e.g. "spmm_segments<bf16,16,1,16>".  Lets tests pin the exact
+ * kernel a benchmark configuration times.  No device work.
+ */
+int lgx_spmm_kernel_name(int64_t d, int dtype, int64_t seg_len, char* buf, size_t len);
 /* Y = A X (alias of lgx_propagate_layer with LGX_LAYER_PLAIN). */
 int lgx_spmm_csr(const lgx_csr* A, const void* X, void* Y, int64_t d, int dtype, lgx_stream_t stream);
 /* Workspace bytes of lgx_propagate: 2 x [N,d] dtype ping-pong tables + [N,d] f32 layer sum. */
@@ -170,6 +176,11 @@ int lgx_score_topk(const void* Q, const int64_t* user_rows, const void* items, i
                    const int32_t* mask_indices, int k, float mask_value, int apply_sigmoid,
                    int32_t* out_idx, float* out_val, float* minmax_out, void* ws,
                    size_t ws_bytes, lgx_stream_t stream);
+/*
+ * Host-only introspection: the launch plan lgx_score_topk uses for (B, n_items, d, dtype, k) --
+ * kernel, user ranges, full-sweep / catalog-split mode -- as text.  No device work.
+ */
+int lgx_score_topk_plan(int64_t B, int64_t n_items, int64_t d, int dtype, int k, char* buf, size_t len);
 /* Row-wise top-k of a dense f32 matrix (row stride ld), ties -> lower column.  k in [1, 256]. */
 int lgx_topk_rows(const float* S, int64_t rows, int64_t cols, int64_t ld, int k, int32_t* out_idx,
                   float* out_val, lgx_stream_t stream);

@@ -35,11 +35,11 @@ def test_version_and_error_channel():
     from factors_of_serendipity_recommendation_amd import _lib
     L = _lib.lib()
     assert b"gfx950" in L.lgx_version()
-    # k outside [1, 64] is rejected before any device work
+    # k outside [1, 256] is rejected before any device work
     rc = L.lgx_topk_rows(None, 1, 10, 10, 0, None, None, None)
     assert rc != 0
-    rc = L.lgx_topk_rows(ctypes.c_void_p(16), 1, 10, 10, 65, ctypes.c_void_p(16), None, None)
-    assert rc == 3 and b"k=65" in L.lgx_last_error()
+    rc = L.lgx_topk_rows(ctypes.c_void_p(16), 1, 10, 10, 257, ctypes.c_void_p(16), None, None)
+    assert rc == 3 and b"k=257" in L.lgx_last_error()
     with pytest.raises(RuntimeError, match="lgx_topk_rows"):
         _lib.check(rc, "lgx_topk_rows")
 

@@ -1,0 +1,141 @@
+"""GPU: the exact kernel instantiations bench.py times, pinned against the oracle.
+
+bench.py's numbers rest on three dispatches; each test below first asserts (through the host-only
+introspection entry points lgx_spmm_kernel_name / lgx_score_topk_plan) that it runs the SAME
+instantiation / launch plan as the benchmark configuration, then checks the result:
+
+  * C4 propagation (BASELINE configs[3], bench default): spmm_segments<bf16,16,1,16> -- d=128 bf16,
+    the seg_len > 128 plan -- and its fp32 twin spmm_segments<f32,32,1,8>, on a hub-heavy graph with
+    seg_len 8192 forced (split rows + fix-up) against oracle.propagate; and the full-size 10M x 1M
+    graph at d=128 in both dtypes through the eigenvector property.
+  * C5 scoring (configs[4]): the LDS kernel in full-sweep mode plus the catalog-split tail launch,
+    d=256 bf16, mask on, checked on the device against float64 scores for sampled users.
+  * C1 (configs[0], Gowalla shape 29,858 x 40,981, 810,128 edges, K=3, d=64 fp32): adjacency
+    bit-exact and propagation against the oracle.
+
+Tolerances as tests/test_gpu_parity.py: fp32 |gpu - oracle| <= 1e-5 |oracle| + 1e-6 max|E0|;
+bf16 storage <= 2e-2 |oracle| + 2e-2 rms(oracle); top-k: k distinct unmasked items, each within
+1e-5 of the exact k-th best (reference: model.py:163-176, Procedure.py:127-135).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+
+import factors_of_serendipity_recommendation_amd as lgx
+from factors_of_serendipity_recommendation_amd import ops
+from factors_of_serendipity_recommendation_amd.graph import choose_seg_len
+from factors_of_serendipity_recommendation_amd.synth import CONFIGS, synth_edges, synth_graph
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+C4 = CONFIGS["synth10m"]
+
+
+def _bf16_round(a):
+    return torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(torch.bfloat16).to(torch.float32).numpy()
+
+
+def _bench_spmm_kernel(dtype):
+    return ops.spmm_kernel_name(C4.d, dtype, choose_seg_len(2 * C4.n_edges))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_c4_spmm_instantiation_on_hub_graph(dtype):
+    """The C4 kernel (d=128, seg_len 8192) on a graph whose hub rows are split into many segments."""
+    rng = np.random.default_rng(404)
+    U, I, E, d = 100_000, 4_000, 1_500_000, C4.d
+    u = rng.integers(0, U, E).astype(np.int32)
+    i = (rng.zipf(1.3, E) % I).astype(np.int32)
+    ip, ix, iv = oracle.build_norm_adj(u, i, U, I, dedup=True)
+    seg = choose_seg_len(2 * C4.n_edges)
+    A = lgx.from_csr_arrays(ip, ix, iv, device=DEV, n_users=U, n_items=I, seg_len=seg)
+    assert A.plan.seg_len == seg == 8192
+    assert int(np.diff(ip).max()) > 4 * seg and len(A.plan.split_row) > 0  # hub rows take the fix-up
+    assert ops.spmm_kernel_name(d, dtype, A.plan.seg_len) == _bench_spmm_kernel(dtype)
+    E0 = (rng.standard_normal((U + I, d)) * 0.1).astype(np.float32)
+    if dtype == torch.bfloat16:
+        E0 = _bf16_round(E0)
+    out = lgx.propagate(A, torch.from_numpy(E0).to(DEV).to(dtype), C4.K).cpu().numpy()
+    ref = oracle.propagate(ip, ix, iv, E0, C4.K)
+    err = np.abs(out - ref)
+    if dtype == torch.bfloat16:
+        tol = 2e-2 * np.abs(ref) + 2e-2 * np.sqrt(np.mean(ref ** 2))
+    else:
+        tol = 1e-5 * np.abs(ref) + 1e-6 * np.abs(E0).max()
+    assert (err <= tol).all(), f"max err {err.max():.3e}"
+
+
+@pytest.mark.slow
+def test_c4_full_size_d128_both_dtypes():
+    """BASELINE configs[3] at full size (10M x 1M, 1e9 nonzeros) and the bench's d=128, in the bench's
+    bf16 storage and in fp32: v = sqrt(deg) is a fixed point of A^ (A^ v = v), so every layer and the
+    layer mean reproduce v column-scaled; rows of degree 0 give 0."""
+    A = synth_graph(C4, 2020, DEV)
+    assert A.nnz == 2 * C4.n_edges
+    deg = torch.diff(A.indptr).double()
+    v = deg.sqrt()
+    col = torch.arange(1, C4.d + 1, device=DEV, dtype=torch.float64) / C4.d
+    for dtype, rel in ((torch.bfloat16, 2e-2), (torch.float32, 1e-4)):
+        assert ops.spmm_kernel_name(C4.d, dtype, A.plan.seg_len) == _bench_spmm_kernel(dtype)
+        E0 = (v[:, None] * col[None, :]).to(dtype)
+        out = lgx.propagate(A, E0, C4.K)
+        ref = E0.float()
+        bad = ((out - ref).abs() > rel * ref.abs() + rel * 1e-3).sum().item()
+        assert bad == 0, f"{dtype}: {bad} entries off the fixed point"
+        del E0, out, ref
+        torch.cuda.empty_cache()
+
+
+def test_c5_scoring_full_sweep_plan_d256():
+    """The C5 launch plan (full-sweep LDS kernel over whole rounds of 256 user tiles, then a
+    catalog-split launch for the 67-tile remainder) at d=256 bf16 with the train mask."""
+    B, I, d, k = 256 * (256 + 67), 100_000, 256, 20
+    plan = ops.score_topk_plan(B, I, d, torch.bfloat16, k)
+    bench = ops.score_topk_plan(1_000_000, 1_000_000, d, torch.bfloat16, k)
+    kinds = [p.split(" users")[0] + " " + p.split(") ")[1].split(" n_splits")[0] for p in plan.split("; ")]
+    bkinds = [p.split(" users")[0] + " " + p.split(") ")[1].split(" n_splits")[0] for p in bench.split("; ")]
+    assert kinds == bkinds and "full-sweep" in plan and len(kinds) == 2, (plan, bench)
+    g = torch.Generator(device=DEV).manual_seed(11)
+    Q = (torch.randn(B, d, device=DEV, generator=g) / 16).bfloat16()
+    items = (torch.randn(I, d, device=DEV, generator=g) / 16).bfloat16()
+    per = 50
+    m = torch.randint(0, I, (B, per), device=DEV, generator=g).sort(1).values
+    keep = torch.ones_like(m, dtype=torch.bool)
+    keep[:, 1:] = m[:, 1:] != m[:, :-1]
+    lens = keep.sum(1)
+    indptr = torch.zeros(B + 1, dtype=torch.int64, device=DEV)
+    indptr[1:] = torch.cumsum(lens, 0)
+    mask = (indptr, m[keep].to(torch.int32))
+    idx, val = lgx.score_topk(Q, items, k, mask=mask)
+    # users from both launches (full-sweep range and the split tail), checked in float64
+    sel = torch.cat([torch.randint(0, 65536, (1500,), device=DEV, generator=g),
+                     torch.randint(65536, B, (1500,), device=DEV, generator=g)])
+    S = Q[sel].double() @ items.double().T
+    for j, u in enumerate(sel.tolist()):
+        S[j, mask[1][indptr[u]:indptr[u + 1]].long()] = float("-inf")
+    kth = torch.topk(S, k, dim=1).values[:, -1:]
+    got_idx = idx[sel].long()
+    assert (got_idx >= 0).all()
+    got = S.gather(1, got_idx)
+    assert torch.isfinite(got).all()
+    assert (got >= kth - 1e-5 * kth.abs().clamp(min=1.0)).all()
+    srt = got_idx.sort(1).values
+    assert (srt[:, 1:] != srt[:, :-1]).all()
+    assert torch.allclose(val[sel].double(), got, rtol=1e-5, atol=1e-5)
+
+
+def test_c1_gowalla_shape_vs_oracle():
+    cfg = CONFIGS["gowalla"]
+    u, i = synth_edges(cfg, 2020, DEV)
+    assert u.numel() == cfg.n_edges
+    A = lgx.build_norm_adj(u, i, cfg.n_users, cfg.n_items, dedup=True, device=DEV)
+    ip, ix, iv = oracle.build_norm_adj(u.cpu().numpy(), i.cpu().numpy(), cfg.n_users, cfg.n_items, dedup=True)
+    assert np.array_equal(A.indptr.cpu().numpy(), ip) and np.array_equal(A.indices.cpu().numpy(), ix)
+    assert np.array_equal(A.vals.cpu().numpy(), iv)
+    E0 = lgx.fill_normal((cfg.n_users + cfg.n_items, cfg.d), 0.1, 2020, device=DEV)
+    out = lgx.propagate(A, E0, cfg.K).cpu().numpy()
+    ref = oracle.propagate(ip, ix, iv, E0.cpu().numpy(), cfg.K)
+    err = np.abs(out - ref)
+    assert (err <= 1e-5 * np.abs(ref) + 1e-6 * float(E0.abs().max())).all(), f"max err {err.max():.3e}"

@@ -1,0 +1,138 @@
+"""GPU: top-k beyond one wave (k up to 256) and the end-to-end ``Procedure.Test`` against the oracle.
+
+  * lgx_topk_rows / lgx_score_topk for k in (65, 100, 200, 256): the reference's top-k has no
+    size limit (tools.h:13-33 partial_sort_copy; torch.topk in Procedure.py:135; TF --Ks up to
+    100, LightGCN-tf/utility/parser.py:59).  topk_rows is bit-exact against the oracle (ties ->
+    lower index); score_topk gives identical sets modulo ties at 1e-5 of the k-th score.
+  * evaluator.Test (Procedure.py:96-174) on mlls, K=3, topks=[20, 100]: the GPU result dict equals
+    the oracle restatement = oracle.propagate (f64) -> oracle.score_topk (sigmoid, mask -(1<<10))
+    -> oracle.torch_style_metrics (utils.getLabel / RecallPrecision_ATk / NDCGatK_r,
+    code/utils.py:218-285) / n_users.  Tolerance: recall / precision equal to 1e-12 (set based);
+    NDCG within 1e-6 relative (an exact fp32 tie between two adjacent positions could swap them).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+
+import factors_of_serendipity_recommendation_amd as lgx
+from factors_of_serendipity_recommendation_amd import evaluator, ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _bf16_round(a):
+    return torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(torch.bfloat16).to(torch.float32).numpy()
+
+
+def _assert_sets(idx, S, k, rel):
+    for r in range(idx.shape[0]):
+        g = set(int(x) for x in idx[r] if x >= 0 and np.isfinite(S[r, x]))
+        order = np.lexsort((np.arange(S.shape[1]), -S[r]))
+        o = [int(x) for x in order[:k] if np.isfinite(S[r, x])]
+        if g == set(o):
+            continue
+        kth = S[r, o[-1]]
+        for x in g ^ set(o):
+            assert abs(S[r, x] - kth) <= rel * max(1.0, abs(kth)), (r, x, S[r, x], kth)
+
+
+@pytest.mark.parametrize("k", [65, 100, 128, 200, 256])
+@pytest.mark.parametrize("cols", [5000, 40_000])
+def test_topk_rows_large_k_bit_exact(k, cols):
+    rng = np.random.default_rng(k + cols)
+    S = rng.standard_normal((37, cols)).astype(np.float32)
+    S[3, :] = 0.5                  # all ties -> lowest indices
+    S[4, 100:400] = 9.0            # ties straddling the k-th slot
+    idx, val = lgx.topk_rows(torch.from_numpy(S).to(DEV), k)
+    oidx, oval = oracle.topk_rows(S, k)
+    assert np.array_equal(idx.cpu().numpy(), oidx)
+    assert np.array_equal(val.cpu().numpy(), oval)
+
+
+@pytest.mark.parametrize("dtype,d", [(torch.float32, 64), (torch.bfloat16, 128), (torch.bfloat16, 256)])
+@pytest.mark.parametrize("k", [65, 100, 200])
+def test_score_topk_large_k_masked(dtype, d, k):
+    """k > 64: the register-fragment kernel (4 waves per workgroup up to k = 128, 1 above) and the
+    two- / four-register finalize merge; small batches split the catalog so several partial lists
+    per user are merged."""
+    rng = np.random.default_rng(7 * k + d)
+    B, I = 150, 6000
+    Q = rng.standard_normal((B, d)).astype(np.float32)
+    items = rng.standard_normal((I, d)).astype(np.float32)
+    if dtype == torch.bfloat16:
+        Q, items = _bf16_round(Q), _bf16_round(items)
+    masks = [np.unique(rng.integers(0, I, rng.integers(0, 80))) for _ in range(B)]
+    mask = ops.lists_to_device_csr(masks, DEV)
+    idx, val = lgx.score_topk(torch.from_numpy(Q).to(DEV).to(dtype), torch.from_numpy(items).to(DEV).to(dtype), k,
+                              mask=mask)
+    S = Q.astype(np.float64) @ items.astype(np.float64).T
+    for u, m in enumerate(masks):
+        S[u, m] = -np.inf
+    idx = idx.cpu().numpy()
+    _assert_sets(idx, S, k, 1e-5)
+    assert all(len(set(r)) == k for r in idx.tolist())
+    got = np.take_along_axis(S, idx.astype(np.int64), 1)
+    assert np.allclose(val.cpu().numpy(), got, rtol=1e-5, atol=1e-5)
+    assert (np.diff(val.cpu().numpy(), axis=1) <= 0).all()  # descending
+
+
+def test_score_topk_large_k_masked_tail():
+    """k = 100 over a 90-item catalog with masks: the masked tail fills slots in index order and slots
+    past the catalog are -1, as for k <= 64."""
+    rng = np.random.default_rng(5)
+    Q = torch.from_numpy(rng.standard_normal((4, 32)).astype(np.float32)).to(DEV)
+    items = torch.from_numpy(rng.standard_normal((90, 32)).astype(np.float32)).to(DEV)
+    masks = [list(range(0, 90, 3)), [], list(range(90)), [5, 6]]
+    mask = ops.lists_to_device_csr(masks, DEV)
+    idx, val = lgx.score_topk(Q, items, 100, mask=mask, mask_value=-1024.0, apply_sigmoid=True)
+    oidx, oval = oracle.score_topk(Q.cpu().numpy(), items.cpu().numpy(), 100, masks, mask_value=-1024.0,
+                                   apply_sigmoid=True)
+    assert np.array_equal(idx.cpu().numpy(), oidx)
+    assert np.allclose(val.cpu().numpy(), oval, rtol=1e-6, atol=1e-7)
+
+
+def _mlls_loader(mlls, tmp_path):
+    from factors_of_serendipity_recommendation_amd.dataloader import Loader
+    tp, tx = mlls["train_list_indptr"], mlls["train_list_indices"]
+    with open(tmp_path / "train.txt", "w") as f:
+        for j, u in enumerate(mlls["train_list_users"]):
+            f.write(" ".join(str(x) for x in [u] + list(tx[tp[j]:tp[j + 1]])) + "\n")
+    sp_, sx = mlls["test_indptr"], mlls["test_indices"]
+    with open(tmp_path / "test.txt", "w") as f:
+        for j, u in enumerate(mlls["test_users"]):
+            f.write(" ".join(str(x) for x in [u] + list(sx[sp_[j]:sp_[j + 1]])) + "\n")
+    return Loader(path=str(tmp_path), device=DEV)
+
+
+def test_procedure_test_matches_oracle_restatement(mlls, tmp_path):
+    from factors_of_serendipity_recommendation_amd.model import LightGCN
+    ds = _mlls_loader(mlls, tmp_path)
+    eu, ei = mlls["emb_user"].astype(np.float32), mlls["emb_item"].astype(np.float32)
+    cfg = {"latent_dim_rec": eu.shape[1], "lightGCN_n_layers": 3, "keep_prob": 0.6, "A_split": False,
+           "pretrain": 1, "user_emb": eu, "item_emb": ei, "dropout": 0}
+    model = LightGCN(cfg, ds).to(DEV)
+    topks = [20, 100]
+    got = evaluator.Test(ds, model, topks=topks)
+
+    # oracle: Procedure.Test restated on the CPU (f64 propagation of the same adjacency)
+    A = ds.getSparseGraph().coalesce().cpu()
+    idx = A.indices().numpy()
+    U, I = ds.n_users, ds.m_items
+    ip = np.zeros(U + I + 1, dtype=np.int64)
+    np.add.at(ip, idx[0] + 1, 1)
+    ip = np.cumsum(ip)
+    prop = oracle.propagate(ip, idx[1].astype(np.int32), A.values().numpy().astype(np.float32),
+                            np.concatenate([eu, ei]), 3)
+    users = list(ds.testDict.keys())
+    allPos = ds.getUserPosItems(users)
+    oidx, _ = oracle.score_topk(prop[:U][users].astype(np.float32), prop[U:].astype(np.float32), max(topks),
+                                [list(p) for p in allPos], mask_value=-float(1 << 10), apply_sigmoid=True)
+    truth = [ds.testDict[u] for u in users]
+    ref = oracle.torch_style_metrics(oidx, truth, topks)
+    for key in ("recall", "precision"):
+        assert np.allclose(got[key], ref[key] / len(users), rtol=0, atol=1e-12), (key, got[key], ref[key])
+    assert np.allclose(got["ndcg"], ref["ndcg"] / len(users), rtol=1e-6, atol=0), (got["ndcg"], ref["ndcg"])
+    assert got["recall"][1] > got["recall"][0] > 0

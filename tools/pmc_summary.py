@@ -49,6 +49,7 @@ def main():
         if os.path.exists(os.path.join(src, name)):
             shutil.copy(os.path.join(src, name), pre + name.replace("bench.json", "bench_line.json")
                         if name == "bench.json" else pre + name)
+    # kernels keyed by workload leg: the bf16 / f32 SpMM instantiations and the scoring kernels
     per = defaultdict(lambda: {"FETCH_SIZE": [], "WRITE_SIZE": []})
     for counter, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
         rows = pmc_rows(os.path.join(src, sub, "**", "*counter_collection.csv"), counter)
@@ -58,20 +59,28 @@ def main():
                 w.writeheader()
                 w.writerows(rows)
         for r in rows:
-            per[short(r["Kernel_Name"])][counter].append(float(r["Counter_Value"]))
-    kernels = {}
-    for k, v in per.items():
+            name = r["Kernel_Name"]
+            k = short(name)
+            leg = "scoring" if "score" in k else ("bf16" if "unsigned short" in name else "f32")
+            per[(leg, k)][counter].append(float(r["Counter_Value"]))
+    kernels = defaultdict(dict)
+    for (leg, k), v in per.items():
         if not v["FETCH_SIZE"] or not v["WRITE_SIZE"]:
             continue
         f = sum(v["FETCH_SIZE"]) / len(v["FETCH_SIZE"])
         w = sum(v["WRITE_SIZE"]) / len(v["WRITE_SIZE"])
-        kernels[k] = {"FETCH_SIZE_KB_mean": f, "WRITE_SIZE_KB_mean": w, "dispatches": len(v["FETCH_SIZE"]),
-                      "hbm_bytes_per_launch": (2 * f + w) * 1024}
-    doc = {"workload": f"{config} (bench.py default: propagation K=3 d=128 bf16 + scoring d=256 bf16, 1M items), "
-                       "n_gpus=1",
+        kernels[leg][k] = {"FETCH_SIZE_KB_mean": f, "WRITE_SIZE_KB_mean": w, "dispatches": len(v["FETCH_SIZE"]),
+                           "hbm_bytes_per_launch": (2 * f + w) * 1024}
+    import hashlib
+    h = hashlib.sha256(open(os.path.join(ROOT, "factors_of_serendipity_recommendation_amd", "liblgx.so"), "rb").read())
+    doc = {"workload": f"{config} (bench.py default: propagation K=3 d=128 bf16 and f32 + scoring d=256 bf16, "
+                       "1M items), n_gpus=1",
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (tools/profile_round.sh); "
-                     "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024, the x2 being the gfx950 FETCH_SIZE "
-                     "correction for 16-B/lane reads",
+                     "bytes = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024, the x2 measured for streaming reads and for "
+                     "random 256-B / 512-B row gathers (profiles/r02_fetch_calibration.json). FETCH_SIZE counts "
+                     "L2 misses served by the Infinity Cache as well as HBM reads (same calibration), so this is "
+                     "L2-miss traffic, an upper bound on HBM traffic",
+           "lib_sha256_16": h.hexdigest()[:16],
            "kernels": kernels}
     with open(pre + "pmc_traffic.json", "w") as fh:
         json.dump(doc, fh, indent=1)
