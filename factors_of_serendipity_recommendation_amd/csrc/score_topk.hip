@@ -34,14 +34,14 @@ namespace {
 // Development statistics (tools/score_stats.hip defines LGX_SCORE_STATS; the library never does):
 // per-wave counters and s_memtime cycle stamps, summed into a device array at the end.
 #ifdef LGX_SCORE_STATS
-__device__ unsigned long long g_score_stats[12];
-#define LGX_STAT_DECL uint64_t stat_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+__device__ unsigned long long g_score_stats[24];
+#define LGX_STAT_DECL uint64_t stat_[24] = {};
 #define LGX_STAT(i, v) (stat_[i] += (v))
 #define LGX_STAT_T0 const uint64_t stat_t0_ = __builtin_amdgcn_s_memtime();
 #define LGX_STAT_T1(i) LGX_STAT(i, __builtin_amdgcn_s_memtime() - stat_t0_);
 #define LGX_STAT_FLUSH                                                                                 \
     if ((threadIdx.x & 63) == 0)                                                                       \
-        for (int i_ = 0; i_ < 12; ++i_) atomicAdd(&g_score_stats[i_], (unsigned long long)stat_[i_]);
+        for (int i_ = 0; i_ < 24; ++i_) atomicAdd(&g_score_stats[i_], (unsigned long long)stat_[i_]);
 #else
 #define LGX_STAT_DECL
 #define LGX_STAT(i, v)
@@ -234,6 +234,10 @@ struct WaveTopK {
 
     // new worst entry: 8 keys (four 16-byte reads issued together) per LDS round trip
     __device__ __forceinline__ void rescan() {
+        LGX_STAT(19, 1);
+#ifdef LGX_SCORE_STATS
+        const uint64_t rs_t0_ = __builtin_amdgcn_s_memtime();
+#endif
         uint64_t m = ~0ull;
         int p = 0;
         for (int j0 = 0; j0 < k; j0 += 8) {
@@ -255,6 +259,9 @@ struct WaveTopK {
         }
         mp = p;
         kmin = m;
+#ifdef LGX_SCORE_STATS
+        stat_[20] += __builtin_amdgcn_s_memtime() - rs_t0_;
+#endif
     }
 
     // consume NACC (1 or 2) 32-item accumulator tiles; tile j's item rows start at i0 + 32 j
@@ -359,9 +366,18 @@ struct WaveTopK {
                 return;
             }
             LGX_STAT(2, 1);
+        } else {
+            LGX_STAT(17, 1);
         }
+#ifdef LGX_SCORE_STATS
+        const uint64_t ex_t0_ = __builtin_amdgcn_s_memtime();
+#endif
         drain(a);
         insert_now<NACC, L16>(a, acc0, acc1, ib, survivors<NACC, L16>(acc0, acc1, ib, rem));
+#ifdef LGX_SCORE_STATS
+        stat_[15] += __builtin_amdgcn_s_memtime() - ex_t0_;
+        stat_[16] += 1;
+#endif
     }
 
     template <bool L16>
@@ -485,6 +501,13 @@ struct WaveTopK {
     // list updates half by half
     __device__ __forceinline__ void drain(const ScoreArgs& a) {
         if (__ballot(pcnt > 0) == 0ull) return;
+#ifdef LGX_SCORE_STATS
+        const uint64_t dr_t0_ = __builtin_amdgcn_s_memtime();
+        struct DrainStamp {
+            uint64_t* acc; uint64_t t0;
+            __device__ ~DrainStamp() { *acc += __builtin_amdgcn_s_memtime() - t0; }
+        } dr_stamp_{&stat_[21], dr_t0_};
+#endif
         const uint32_t keep = drop_masked(a);
         for (int ph = 0; ph < 2; ++ph) {
             if (__ballot(ph == h && pcnt > 0) == 0ull) continue;
@@ -506,6 +529,7 @@ struct WaveTopK {
             if (ph == h) {
                 uint32_t todo = cmask;
                 while (todo) {  // one copy of the insertion code, one iteration per survivor
+                    LGX_STAT(18, 1);
                     const int r = __builtin_ctz(todo);
                     todo &= todo - 1;
                     insert_key<true>(a, make_key(pick<NACC>(acc0, acc1, r), item_of<L16>(ib, r)));
@@ -659,10 +683,15 @@ __device__ __forceinline__ uint32_t lds_u32(const void* p) {
 // v_permlane16_swap per accumulator register then regroups them so that lane l holds 32 scores of
 // user l & 31 (items 16 q + 8 h + 0..7 of block q), the layout the top-k state expects: lanes l and
 // l + 32 still share a user.
-template <int KSTEPS, bool MINMAX, int ABLATE = 0, int WAVES = 8, int NACC = 2, bool STAGGER = true, bool M16 = true>
+template <int KSTEPS, bool MINMAX, int ABLATE = 0, int WAVES = 8, int NACC = 2, bool STAGGER = true, bool M16 = true,
+          int DMAPOS = 0, bool FASTSKIP = true>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf) {
     static_assert(!M16 || (NACC == 2 && KSTEPS % 2 == 0), "16x16x32 path: 64-item tiles, d a multiple of 32");
+    // SKIP: the fast-path test runs on the MFMA output layout itself (lane l holds 16 scores of user
+    // l & 15 and 16 of user 16 + (l & 15)); the regroup into the top-k layout (16 v_permlane16_swap)
+    // is paid only by tiles that have a survivor.  Min / max needs every score: not with MINMAX.
+    constexpr bool SKIP = FASTSKIP && M16 && !MINMAX && ABLATE == 0;
     typedef LdsGeom<KSTEPS, WAVES, NACC> G;
     typedef Frag<LGX_DTYPE_BF16> F;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -740,22 +769,27 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
         if (u >= ntiles) u -= ntiles;
         return i_begin + u * G::TILE_ITEMS;
     };
-    auto stage = [&](int buf, int64_t t0) {
-        const unsigned char* base = items + t0 * G::RB;
-        const bool tail = t0 + G::TILE_ITEMS > i_end;
-        const int last = (int)(i_end - 1 - t0);  // tail rows re-read the split's last row (masked later)
-#pragma unroll
-        for (int p = 0; p < G::PPW; ++p) {
-            if (p < my_pieces) {
-                // offsets recomputed per tile: cheaper than holding them in registers
-                const int q = (wave * G::PPW + p) * 64 + lane;
-                const int row = q / G::CPR;
-                const int src = (q % G::CPR) ^ (row & G::SWZ);
-                const int srow = tail && row > last ? last : row;
-                lds_dma16(base, (uint32_t)(srow * G::RB + src * 16),
-                          __builtin_amdgcn_readfirstlane(lds_tiles + buf * G::TILE + (wave * G::PPW + p) * 1024));
-            }
+    auto stage_piece = [&](int buf, int64_t t0, int p) {
+        if (p < my_pieces) {
+            // wave-uniform by construction; readfirstlane keeps the base in SGPRs for the asm operand
+            const uint64_t bu = reinterpret_cast<uint64_t>(items + t0 * G::RB);
+            const unsigned char* base = reinterpret_cast<const unsigned char*>(
+                ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(bu >> 32)) << 32) |
+                (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)bu));
+            const bool tail = t0 + G::TILE_ITEMS > i_end;
+            const int last = (int)(i_end - 1 - t0);  // tail rows re-read the split's last row (masked later)
+            // offsets recomputed per tile: cheaper than holding them in registers
+            const int q = (wave * G::PPW + p) * 64 + lane;
+            const int row = q / G::CPR;
+            const int src = (q % G::CPR) ^ (row & G::SWZ);
+            const int srow = tail && row > last ? last : row;
+            lds_dma16(base, (uint32_t)(srow * G::RB + src * 16),
+                      __builtin_amdgcn_readfirstlane(lds_tiles + buf * G::TILE + (wave * G::PPW + p) * 1024));
         }
+    };
+    auto stage = [&](int buf, int64_t t0) {
+#pragma unroll
+        for (int p = 0; p < G::PPW; ++p) stage_piece(buf, t0, p);
     };
 
     const int ahead = nbuf - 1;
@@ -765,14 +799,45 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
     int buf = 0, sbuf = ahead;  // buffer of tile t / of tile t + ahead
     const bool late = STAGGER && ABLATE == 0 && wave >= WAVES / 2;  // wave-uniform
     f32x16 acc0, acc1;  // late waves: tile t-1's scores, held across the barrier
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    f32x4 c[2][4];      // 16x16x32 accumulators: c[ub][ib] = items 16 ib + 4 (lane >> 4) + reg, user 16 ub + (lane & 15)
     int64_t prev_t0 = 0;
+    // SKIP: the thresholds of this lane's two MFMA-layout users (refreshed after every event)
+    float tauA = st.tau, tauB = st.tau;
+    auto refresh_taus = [&]() {
+        tauA = __shfl(st.tau, lane & 15);
+        tauB = __shfl(st.tau, 16 + (lane & 15));
+    };
+    if (SKIP) refresh_taus();
+    // regroup: swap(X = user block 0, Y = user block 1) between rows 2m and 2m+1 (lanes l, l^16)
+    // leaves X' = items 16 ib + 8 h + reg, Y' = items 16 ib + 8 h + 4 + reg of user l & 31
+    auto regroup = [&]() {
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib) {
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(c[0][ib][reg]),
+                                                                 __float_as_uint(c[1][ib][reg]), false, false);
+                const int r = 8 * (ib & 1) + reg;
+                if (ib < 2) {
+                    acc0[r] = __uint_as_float(sw[0]);
+                    acc0[r + 4] = __uint_as_float(sw[1]);
+                } else {
+                    acc1[r] = __uint_as_float(sw[0]);
+                    acc1[r + 4] = __uint_as_float(sw[1]);
+                }
+            }
+        }
+    };
     // scores of the tile in ring buffer `buf` into acc0 / acc1 (the same code for both wave kinds)
+    // DMAPOS 1: the refill pieces of tile t + ahead are issued between the k-steps of tile t's MFMAs
+    // (piece p after k-step p) instead of all at once before them
+    bool refill = false;
+    int64_t refill_t0 = 0;
     auto compute = [&]() {
         const unsigned char* T = tiles + buf * G::TILE;
         if constexpr (M16) {
             constexpr int KS2 = KSTEPS / 2;
-            typedef float f32x4 __attribute__((ext_vector_type(4)));
-            f32x4 c[2][4];
 #pragma unroll
             for (int ub = 0; ub < 2; ++ub)
 #pragma unroll
@@ -798,6 +863,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
                             c[ub][ib], 0, 0, 0);
                     if (s2 + 1 < KS2) fa[ib] = frag(s2 + 1, ib);
                 }
+                if (DMAPOS == 1 && s2 < G::PPW && refill) stage_piece(sbuf, refill_t0, s2);
             }
             __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
@@ -808,24 +874,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
                     if (s2 + 1 < KS2) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 }
             }
-            // regroup: swap(X = user block 0, Y = user block 1) between rows 2m and 2m+1 (lanes l, l^16)
-            // leaves X' = items 16 ib + 8 h + reg, Y' = items 16 ib + 8 h + 4 + reg of user l & 31
-#pragma unroll
-            for (int ib = 0; ib < 4; ++ib) {
-#pragma unroll
-                for (int reg = 0; reg < 4; ++reg) {
-                    const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(c[0][ib][reg]),
-                                                                     __float_as_uint(c[1][ib][reg]), false, false);
-                    const int r = 8 * (ib & 1) + reg;
-                    if (ib < 2) {
-                        acc0[r] = __uint_as_float(sw[0]);
-                        acc0[r + 4] = __uint_as_float(sw[1]);
-                    } else {
-                        acc1[r] = __uint_as_float(sw[0]);
-                        acc1[r + 4] = __uint_as_float(sw[1]);
-                    }
-                }
-            }
+            if (!SKIP) regroup();
         } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -861,21 +910,45 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
         }
         }
     };
+    // the split's last tile is the only one that can run past i_end: a block variant of its own
+    auto epilogue = [&](int64_t e0) {
+        const bool tail = e0 + G::TILE_ITEMS > i_end;
+        if constexpr (SKIP) {
+            if (!tail) {
+                float m0 = c[0][0][0], m1 = c[1][0][0];
+#pragma unroll
+                for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        m0 = fmaxf(m0, c[0][ib][r]);
+                        m1 = fmaxf(m1, c[1][ib][r]);
+                    }
+                if (__ballot((m0 >= tauA) | (m1 >= tauB)) == 0ull) return;  // wave-uniform fast path
+            }
+            regroup();
+        }
+        if (tail) st.template block<MINMAX, NACC, false, M16, true>(a, acc0, acc1, e0, i_end);
+        else st.template block<MINMAX, NACC, false, M16, false>(a, acc0, acc1, e0, i_end);
+        if (SKIP) refresh_taus();
+    };
     for (int64_t t = 0; t < ntiles; ++t) {
         LGX_STAT_T0
         const int64_t t0 = tile_start(t);
-        if (ABLATE != 5 && t + ahead < ntiles) stage(sbuf, tile_start(t + ahead));
-        // the split's last tile is the only one that can run past i_end: a block variant of its own
-        auto epilogue = [&](int64_t e0) {
-            if (e0 + G::TILE_ITEMS > i_end) st.template block<MINMAX, NACC, false, M16, true>(a, acc0, acc1, e0, i_end);
-            else st.template block<MINMAX, NACC, false, M16, false>(a, acc0, acc1, e0, i_end);
-        };
+        refill = ABLATE != 5 && t + ahead < ntiles;
+        if (refill) refill_t0 = tile_start(ABLATE == 6 ? 0 : t + ahead);  // 6 (development): L2-hot refills
+        if (DMAPOS == 0 && refill) stage(sbuf, refill_t0);
+#ifdef LGX_SCORE_STATS
+        const uint64_t ep_t0_ = __builtin_amdgcn_s_memtime();
+#endif
         if (late && t > 0) epilogue(prev_t0);
+#ifdef LGX_SCORE_STATS
+        st.stat_[t < 1024 ? 3 : 11] += __builtin_amdgcn_s_memtime() - ep_t0_;
+#endif
         compute();
 #ifdef LGX_SCORE_STATS
         const uint64_t stat_t1_ = __builtin_amdgcn_s_memtime();
 #endif
-        if (ABLATE == 1 || ABLATE == 5) {  // development: MFMA + LDS pipeline only (5: no refills either) (keeps the accumulators live)
+        if (ABLATE == 1 || ABLATE == 5 || ABLATE == 6) {  // development: MFMA + LDS pipeline only (5: no refills either) (keeps the accumulators live)
             float z = 0.0f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) z += acc0[r] + (NACC == 2 ? acc1[r] : 0.0f);
@@ -883,7 +956,13 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
         } else if (ABLATE == 3) {  // development: filter fast path only
             st.template block<MINMAX, NACC, true, M16>(a, acc0, acc1, t0, i_end);
         } else if (!late) {
+#ifdef LGX_SCORE_STATS
+            const uint64_t ep_t1_ = __builtin_amdgcn_s_memtime();
+#endif
             epilogue(t0);
+#ifdef LGX_SCORE_STATS
+            st.stat_[t < 1024 ? 3 : 11] += __builtin_amdgcn_s_memtime() - ep_t1_;
+#endif
         }
         prev_t0 = t0;
 #ifdef LGX_SCORE_STATS
@@ -896,12 +975,13 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
         wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(t + ahead, ntiles - 1) - (t + 1)));
         __syncthreads();
 #ifdef LGX_SCORE_STATS
-        st.stat_[6] += __builtin_amdgcn_s_memtime() - stat_t2_;  // wait + barrier
+        st.stat_[t < 1024 ? 12 : 6] += __builtin_amdgcn_s_memtime() - stat_t2_;  // wait + barrier
+        st.stat_[t < 1024 ? 13 : 14] += 1;
 #endif
         buf = buf + 1 == nbuf ? 0 : buf + 1;
         sbuf = sbuf + 1 == nbuf ? 0 : sbuf + 1;
     }
-    if (late && ntiles > 0) st.template block<MINMAX, NACC, false, M16>(a, acc0, acc1, prev_t0, i_end);
+    if (late && ntiles > 0) epilogue(prev_t0);
     st.flush(a, split, lane);
 #ifdef LGX_SCORE_STATS
     { uint64_t* stat_ = st.stat_; LGX_STAT_FLUSH }
@@ -1225,16 +1305,16 @@ inline int lds_ring_buffers(size_t tile, size_t lists, int wg_per_cu) {
     return (int)std::max<size_t>(2, std::min<size_t>(4, fit));
 }
 
-template <int KS, bool MM, int ABL, int WAVES, int NACC, bool STAGGER, bool M16>
+template <int KS, bool MM, int ABL, int WAVES, int NACC, bool STAGGER, bool M16, int DMAPOS = 0, bool SKIP = true>
 int launch_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     typedef LdsGeom<KS, WAVES, NACC> G;
     const size_t lists = (size_t)WAVES * list_bytes_per_wave(a.k);
     const int nbuf = lds_ring_buffers(G::TILE, lists, WAVES == 4 ? 2 : 1);
     const size_t shmem = (size_t)nbuf * G::TILE + lists;
-    int rc = set_lds_limit(score_topk_bf16_lds<KS, MM, ABL, WAVES, NACC, STAGGER, M16>, shmem);
+    int rc = set_lds_limit(score_topk_bf16_lds<KS, MM, ABL, WAVES, NACC, STAGGER, M16, DMAPOS, SKIP>, shmem);
     if (rc) return rc;
     const unsigned grid = (unsigned)(p.n_utiles * p.n_splits);
-    score_topk_bf16_lds<KS, MM, ABL, WAVES, NACC, STAGGER, M16><<<grid, WAVES * 64, shmem, stream>>>(
+    score_topk_bf16_lds<KS, MM, ABL, WAVES, NACC, STAGGER, M16, DMAPOS, SKIP><<<grid, WAVES * 64, shmem, stream>>>(
         a, p.xcd_affine ? 1 : 0, p.n_utiles, nbuf);
     LGX_LAUNCH_CHECK();
     return LGX_OK;

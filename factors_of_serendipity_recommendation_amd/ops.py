@@ -113,8 +113,12 @@ def score_dense(Q: torch.Tensor, items: torch.Tensor, user_rows: Optional[torch.
 
 
 def lists_to_device_csr(lists: Sequence[Sequence[int]], device, sort: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Ragged python lists -> (indptr int64 [n+1], indices int32) on the device."""
+    """Ragged python lists -> (indptr int64 [n+1], indices int32) on the device.  A
+    ``dataloader.PosLists`` (already sorted and de-duplicated) is packed on the device directly."""
     import numpy as np
+    if hasattr(lists, "device_csr"):
+        ip, ix = lists.device_csr(device)
+        return ip, ix.to(torch.int32)
     lens = np.fromiter((len(l) for l in lists), dtype=np.int64, count=len(lists))
     indptr = np.zeros(len(lists) + 1, dtype=np.int64)
     np.cumsum(lens, out=indptr[1:])

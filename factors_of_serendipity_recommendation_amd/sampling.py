@@ -72,13 +72,14 @@ def sample_negative(user_num: int, item_num: int, train_num: int, allPos, neg_nu
                     device="cuda") -> np.ndarray:
     """sources/sampling.cpp:27-56: train_num // user_num rows per user -> int32 [rows, neg_num + 2]."""
     per = max(1, train_num // max(1, user_num))
-    pos = _positives(list(allPos)[:user_num], device)
+    pos = _positives(allPos.select(range(user_num)) if hasattr(allPos, "select") else list(allPos)[:user_num],
+                     device)
     return sample_device(pos, item_num, per_user=per, neg_num=neg_num).cpu().numpy()
 
 
 def sample_negative_ByUser(users, item_num: int, allPos, neg_num: int, device="cuda") -> np.ndarray:
     """sources/sampling.cpp:58-86: one row per listed user -> int32 [len(users), neg_num + 2]."""
-    pos = _positives(list(allPos), device)
+    pos = _positives(allPos if hasattr(allPos, "device_csr") else list(allPos), device)
     u = torch.as_tensor(np.asarray(users, dtype=np.int32), device=device)
     return sample_device(pos, item_num, users=u, neg_num=neg_num).cpu().numpy()
 

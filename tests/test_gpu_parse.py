@@ -60,12 +60,21 @@ def test_parse_multichunk_random():
     _check(text)
 
 
-def test_loader_files_match_host_reader(mlls, tmp_path):
+def test_loader_files_match_oracle_parser(mlls, tmp_path):
+    """The GPU reader against the oracle's restatement of Loader.__init__ (dataloader.py:247-285)."""
+    from oracle import oracle
     tp, tx = mlls["train_list_indptr"], mlls["train_list_indices"]
     path = tmp_path / "train.txt"
     with open(path, "w") as f:
         for j, u in enumerate(mlls["train_list_users"]):
             f.write(" ".join(str(x) for x in [u] + list(tx[tp[j]:tp[j + 1]])) + "\n")
-    hu, hr = read_interactions(str(path))
+    sp_, sx = mlls["test_indptr"], mlls["test_indices"]
+    tpath = tmp_path / "test.txt"
+    with open(tpath, "w") as f:
+        for j, u in enumerate(mlls["test_users"]):
+            f.write(" ".join(str(x) for x in [u] + list(sx[sp_[j]:sp_[j + 1]])) + "\n")
+    ou, oi, otest, on_u, on_i, otrain = oracle.parse_lightgcn_txt(str(path), str(tpath))
     gu, gr = read_interactions(str(path), DEV)
-    assert hu == gu and len(hr) == len(gr) and all(np.array_equal(a, b) for a, b in zip(hr, gr))
+    assert gu == list(otrain.keys())
+    assert all(np.array_equal(r, otrain[u]) for u, r in zip(gu, gr))
+    assert np.array_equal(np.concatenate(gr), np.asarray(oi))

@@ -1,0 +1,77 @@
+// Development: A/B timing of score_topk_bf16_lds variants on the C5 shape (B users x 1M items,
+// d=256, top-20, 50 masked items per user), launched directly (no finalize), hipEvents, best of 3.
+//   make -C tools score_lab && tools/score_lab [B]
+#include "../factors_of_serendipity_recommendation_amd/csrc/score_topk.hip"
+
+#include <cstdio>
+#include <random>
+#include <vector>
+
+#define HK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { std::printf("%s -> %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
+
+template <int ABL, int DMAPOS, bool SKIP = true, bool STAG = true>
+int launch(const ScoreArgs& a, const SplitPlan& p, hipStream_t s) {
+    return launch_lds_kernel<16, false, ABL, 8, 2, STAG, true, DMAPOS, SKIP>(a, p, s);
+}
+
+int main(int argc, char** argv) {
+    const int64_t B = argc > 1 ? std::atoll(argv[1]) : 131072;
+    const int64_t I = 1000000, d = 256, M = 50;
+    const int k = 20;
+    void *Q, *items, *ws;
+    int32_t* mi;
+    int64_t* mp;
+    HK(hipMalloc(&Q, B * d * 2));
+    HK(hipMalloc(&items, I * d * 2));
+    if (lgx_fill_normal(Q, B * d, 1.0f / 16, 2, LGX_DTYPE_BF16, nullptr)) return 1;
+    if (lgx_fill_normal(items, I * d, 1.0f / 16, 1, LGX_DTYPE_BF16, nullptr)) return 1;
+    std::vector<int64_t> hp(B + 1);
+    std::vector<int32_t> hi(B * M);
+    std::mt19937_64 rng(5);
+    for (int64_t b = 0; b < B; ++b) {
+        hp[b] = b * M;
+        for (int j = 0; j < M; ++j) hi[b * M + j] = (int32_t)(rng() % I);
+        std::sort(hi.begin() + b * M, hi.begin() + (b + 1) * M);
+    }
+    hp[B] = B * M;
+    HK(hipMalloc(&mp, (B + 1) * 8));
+    HK(hipMalloc(&mi, B * M * 4));
+    HK(hipMemcpy(mp, hp.data(), (B + 1) * 8, hipMemcpyHostToDevice));
+    HK(hipMemcpy(mi, hi.data(), B * M * 4, hipMemcpyHostToDevice));
+    const SplitPlan p = plan_splits(B, I, LGX_DTYPE_BF16, d, k);
+    HK(hipMalloc(&ws, (size_t)B * p.n_splits * k * 8 + 4096));
+    hipEvent_t e0, e1;
+    HK(hipEventCreate(&e0));
+    HK(hipEventCreate(&e1));
+    std::printf("B=%lld splits=%d utiles=%lld\n", (long long)B, p.n_splits, (long long)p.n_utiles);
+    const bool dyn = false;
+    auto timeit = [&](const char* name, auto fn, bool masked) -> int {
+        ScoreArgs a{Q, nullptr, items, B, I, d, masked ? mp : nullptr, masked ? mi : nullptr, k, p.n_splits,
+                    p.split_items, reinterpret_cast<float*>(ws),
+                    reinterpret_cast<int32_t*>(static_cast<char*>(ws) + (size_t)B * p.n_splits * k * 4), nullptr};
+        if (fn(a, p, nullptr)) { std::printf("%s: launch failed: %s\n", name, lgx_last_error()); return 1; }
+        float best = 1e30f;
+        for (int r = 0; r < 3; ++r) {
+            HK(hipEventRecord(e0, nullptr));
+            fn(a, p, nullptr);
+            HK(hipEventRecord(e1, nullptr));
+            HK(hipEventSynchronize(e1));
+            float ms;
+            HK(hipEventElapsedTime(&ms, e0, e1));
+            best = std::min(best, ms);
+        }
+        std::printf("%s%-30s masked=%d %9.2f ms %7.0f TF/s\n", dyn ? "dyn " : "    ", name, (int)masked, best, 2.0 * B * I * d / (best * 1e-3) / 1e12);
+        std::fflush(stdout);
+        return 0;
+    };
+    for (int masked = 1; masked >= 0; --masked) {
+        if (timeit("full regroup-always", launch<0, 0, false>, masked)) return 1;
+        if (timeit("full fast-skip", launch<0, 0, true>, masked)) return 1;
+    }
+    if (timeit("no-topk", launch<1, 0>, false)) return 1;
+    if (timeit("no-topk dma@kstep", launch<1, 1>, false)) return 1;
+    if (timeit("no-topk no-refill", launch<5, 0>, false)) return 1;
+    if (timeit("no-topk L2-hot refill", launch<6, 0>, false)) return 1;
+    std::printf("done\n");
+    return 0;
+}

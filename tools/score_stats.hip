@@ -50,19 +50,19 @@ int main(int argc, char** argv) {
     };
     CK(run());
     HK(hipDeviceSynchronize());
-    unsigned long long zero[12] = {0};
+    unsigned long long zero[24] = {0};
     HK(hipMemcpyToSymbol(HIP_SYMBOL(lgx::g_score_stats), zero, sizeof(zero)));
     const auto t0 = std::chrono::steady_clock::now();
     CK(run());
     HK(hipDeviceSynchronize());
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    unsigned long long st[12];
+    unsigned long long st[24];
     HK(hipMemcpyFromSymbol(st, HIP_SYMBOL(lgx::g_score_stats), sizeof(st)));
     const double waves = (double)((B + 255) / 256) * 8;
     std::printf("B=%lld masked=%d: %.1f ms (%.0f TF/s, stats build)\n", (long long)B, (int)masked, ms,
                 2.0 * B * I * d / (ms * 1e-3) / 1e12);
-    const char* names[12] = {"tiles", "events", "drains", "insert_now", "cyc topk", "cyc stage+mfma", "cyc wait+barrier", "cyc events", "mask tests", "exact searches", "cyc searches", "-"};
-    for (int i = 0; i < 11; ++i) std::printf("  per wave %-18s %14.1f\n", names[i], st[i] / waves);
+    const char* names[25] = {"tiles", "events", "drains", "cyc epi t<1024", "cyc topk", "cyc stage+mfma", "cyc wait+bar t>=1024", "cyc events", "mask tests", "exact searches", "cyc searches", "cyc epi t>=1024", "cyc wait+bar t<1024", "tiles t<1024", "tiles t>=1024", "cyc exact path", "exact path entries", "exact (lists filling)", "insert_now iters (lane 0)", "rescans (lane 0)", "cyc rescans", "cyc drains", "-", "-"};
+    for (int i = 0; i < 22; ++i) std::printf("  per wave %-18s %14.1f\n", names[i], st[i] / waves);
     std::printf("  per tile: topk %.0f  stage+mfma %.0f  wait+barrier %.0f cycles (s_memtime units)\n",
                 (double)st[4] / st[0], (double)st[5] / st[0], (double)st[6] / st[0]);
     return 0;
