@@ -430,6 +430,8 @@ def main():
         "config": {"workload": f"{cfg.name}: {cfg.n_users} users x {cfg.n_items} items, {cfg.n_edges} edges "
                                f"(nnz {res['nnz']}), K={cfg.K}, d={cfg.d}, {res['dtype']} storage / fp32 accumulate",
                    "parallelism": f"row-shard{world}" if world > 1 else "single"},
+        "process_group": ({"world_size": dist.get_world_size(), "backend": dist.get_backend()} if world > 1
+                          else None),
         "roofline": res["roofline"], "cpu_baseline": cpu, "fp32": fp32, "scoring": scoring,
     }
     if rank == 0:
