@@ -111,7 +111,20 @@ struct ScoreArgs {
     float* part_score;    // [B, n_splits, k]
     int32_t* part_idx;    // [B, n_splits, k]
     uint32_t* minmax;     // ordered {min, max} or nullptr
+    uint64_t* susp;       // [B, 2, kSuspSlots] parked keys (LDS kernel, full sweep), or nullptr
 };
+
+// Candidates whose mask test the Bloom filter cannot settle ("suspects", ~10 % of the survivors) are
+// parked in the workspace and settled by exact searches once, at the flush: an exact search in the
+// sweep is a chain of dependent global loads that also waits for the in-flight tile DMA (vmcnt
+// completes in order), and the per-tile barrier makes every wave of the workgroup wait for it.  A
+// lane with all its slots taken searches at once, as before.
+constexpr int kSuspSlots = 24;
+#ifndef LGX_BLOOM_WORDS
+#define LGX_BLOOM_WORDS 8
+#endif
+constexpr int kBloomWords = LGX_BLOOM_WORDS;  // 256-bit filter: 8 VGPRs
+constexpr int kBloomShift = 32 - 5 - (kBloomWords == 16 ? 4 : kBloomWords == 8 ? 3 : 2);
 
 __device__ __forceinline__ bool is_masked(const ScoreArgs& a, int64_t b, int32_t item) {
     if (!a.mask_indptr) return false;
@@ -134,8 +147,9 @@ __host__ __device__ constexpr int kstride(int k) { return (k + 1) & ~1; }
 constexpr int kListSpare = 8;  // the 8-key rescan of user 31 may read past its row
 constexpr int kPendSlots = 4;
 __host__ __device__ constexpr size_t list_keys_per_wave(int k) { return (size_t)kUsersPerWave * kstride(k) + kListSpare; }
+// ... then one int per lane: the count of its parked keys (kSuspSlots)
 __host__ __device__ constexpr size_t list_bytes_per_wave(int k) {
-    return (list_keys_per_wave(k) + 64 * (kPendSlots + 1)) * 8;
+    return (list_keys_per_wave(k) + 64 * (kPendSlots + 1)) * 8 + 64 * 4;
 }
 
 // value held by lane (lane ^ 32): one v_permlane32_swap, no LDS traffic
@@ -168,31 +182,50 @@ struct WaveTopK {
     float tau;       // filter threshold: -inf until the list is full, +inf for padding users
     int32_t tau_i;
     float mn, mx;
-    // 512-bit Bloom filter of the user's masked items (2 hashes; false-positive rate ~3% at 50
+    bool park;       // parked keys enabled (full-sweep LDS kernel with a mask); count in LDS (scnt())
+    // 256-bit Bloom filter of the user's masked items (2 hashes; false-positive rate ~10% at 50
     // masked items), as 16 scalars so that the word select stays in registers
-    uint32_t bl[16];
+    uint32_t bl[kBloomWords];
 
-    __device__ __forceinline__ static uint32_t bloom_h1(int32_t x) { return ((uint32_t)x * 0x9E3779B1u) >> 23; }
-    __device__ __forceinline__ static uint32_t bloom_h2(int32_t x) { return ((uint32_t)x * 0x85EBCA77u) >> 23; }
+    __device__ __forceinline__ static uint32_t bloom_h1(int32_t x) { return ((uint32_t)x * 0x9E3779B1u) >> kBloomShift; }
+    __device__ __forceinline__ static uint32_t bloom_h2(int32_t x) { return ((uint32_t)x * 0x85EBCA77u) >> kBloomShift; }
     __device__ __forceinline__ bool bloom_test(uint32_t hv) const {
         // AND with per-word masks: no select over loaded members (which the compiler would turn
         // into a load through a selected pointer and force the state into scratch)
         const uint32_t q = hv >> 5, m = 1u << (hv & 31);
         uint32_t hit = 0;
 #pragma unroll
-        for (int w = 0; w < 16; ++w) hit |= bl[w] & (q == (uint32_t)w ? m : 0u);
+        for (int w = 0; w < kBloomWords; ++w) hit |= bl[w] & (q == (uint32_t)w ? m : 0u);
         return hit != 0u;
     }
     __device__ __forceinline__ void bloom_set(uint32_t hv) {
         const uint32_t q = hv >> 5, m = 1u << (hv & 31);
 #pragma unroll
-        for (int w = 0; w < 16; ++w) bl[w] |= q == (uint32_t)w ? m : 0u;
+        for (int w = 0; w < kBloomWords; ++w) bl[w] |= q == (uint32_t)w ? m : 0u;
     }
-    // exact test only when the filter cannot rule the item out
-    __device__ __forceinline__ bool masked(const ScoreArgs& a, int32_t it) {
+    // true when the key must not enter the list now: masked, or parked for the flush's exact test
+    // (the exact test runs at once only when the filter cannot rule the item out and no slot is free)
+    __device__ __forceinline__ bool masked(const ScoreArgs& a, uint64_t key) {
+        const int32_t it = key_index(key);
         if (!a.mask_indptr) return false;
+#if defined(LGX_MASK_ABL) && LGX_MASK_ABL == 1  // development (tools/score_lab): no mask test at all
+        return false;
+#endif
         LGX_STAT(8, 1);
         if (!bloom_test(bloom_h1(it)) || !bloom_test(bloom_h2(it))) return false;
+#if defined(LGX_MASK_ABL) && LGX_MASK_ABL == 2  // development: Bloom filter only, no exact search
+        return false;
+#endif
+        if (park) {
+            const int c = *scnt();
+            if (c < kSuspSlots) {
+#if !defined(LGX_MASK_ABL) || LGX_MASK_ABL != 3  // 3 (development): parking without the store
+                susp_slots(a)[c] = key;
+#endif
+                *scnt() = c + 1;
+                return true;
+            }
+        }
         LGX_STAT(9, 1);
 #ifdef LGX_SCORE_STATS
         const uint64_t t0_ = __builtin_amdgcn_s_memtime();
@@ -205,7 +238,7 @@ struct WaveTopK {
     }
     __device__ __forceinline__ void build_bloom(const ScoreArgs& a) {
 #pragma unroll
-        for (int w = 0; w < 16; ++w) bl[w] = 0u;
+        for (int w = 0; w < kBloomWords; ++w) bl[w] = 0u;
         if (!a.mask_indptr || !user_ok) return;
         const int64_t m0 = a.mask_indptr[b], m1 = a.mask_indptr[b + 1];
         for (int64_t j = m0; j < m1; ++j) {
@@ -230,6 +263,21 @@ struct WaveTopK {
         tau_i = 0x7fffffff;
         mn = INFINITY;
         mx = -INFINITY;
+        park = false;
+    }
+    // full-sweep launches only (one workgroup per user); split lists test at once
+    __device__ __forceinline__ void enable_suspects(const ScoreArgs& a) {
+        park = a.susp && a.mask_indptr && a.n_splits == 1;  // wave-uniform
+        if (park) *scnt() = 0;
+    }
+    // this lane's parked-key count: the int after the wave's pending slots (list_bytes_per_wave)
+    __device__ __forceinline__ int* scnt() const {
+        const int l = (int)(threadIdx.x & 63);
+        return reinterpret_cast<int*>(pend + (64 - l) * (kPend + 1)) + l;
+    }
+    // recomputed on use (rare) instead of held in registers
+    __device__ __forceinline__ uint64_t* susp_slots(const ScoreArgs& a) const {
+        return a.susp + ((size_t)b * 2 + h) * kSuspSlots;
     }
 
     // new worst entry: 8 keys (four 16-byte reads issued together) per LDS round trip
@@ -424,11 +472,11 @@ struct WaveTopK {
     __device__ __forceinline__ void insert_key(const ScoreArgs& a, uint64_t key) {
         const int32_t it = key_index(key);
         if (len == k) {
-            if (key <= kmin || (CHECK && masked(a, it))) return;
+            if (key <= kmin || (CHECK && masked(a, key))) return;
             keys[mp] = key;
             rescan();
         } else {
-            if (CHECK && masked(a, it)) return;
+            if (CHECK && masked(a, key)) return;
             keys[len++] = key;
             if (len == k) rescan();
         }
@@ -440,6 +488,9 @@ struct WaveTopK {
     __device__ __forceinline__ uint32_t drop_masked(const ScoreArgs& a) {
         uint32_t keep = (1u << pcnt) - 1u;
         if (!a.mask_indptr) return keep;
+#if defined(LGX_MASK_ABL) && LGX_MASK_ABL == 1
+        return keep;
+#endif
         int32_t it[kPend];
         uint32_t need = 0;
 #pragma unroll
@@ -448,6 +499,24 @@ struct WaveTopK {
             if (j < pcnt && bloom_test(bloom_h1(it[j])) && bloom_test(bloom_h2(it[j]))) need |= 1u << j;
         }
         if (__ballot(need != 0u) == 0ull) return keep;
+#if defined(LGX_MASK_ABL) && LGX_MASK_ABL == 2
+        return keep;
+#endif
+        if (park) {  // park them while slots last
+            int c = *scnt();
+            for (int j = 0; j < kPend; ++j) {
+                if (((need >> j) & 1u) && c < kSuspSlots) {
+#if !defined(LGX_MASK_ABL) || LGX_MASK_ABL != 3
+                    susp_slots(a)[c] = pend_key(pend[j]);
+#endif
+                    ++c;
+                    keep &= ~(1u << j);
+                    need &= ~(1u << j);
+                }
+            }
+            *scnt() = c;
+            if (__ballot(need != 0u) == 0ull) return keep;
+        }
         LGX_STAT(9, 1);
         const int64_t m0 = need ? a.mask_indptr[b] : 0, m1 = need ? a.mask_indptr[b + 1] : 0;
         const int32_t* mi = a.mask_indices + m0;
@@ -545,8 +614,33 @@ struct WaveTopK {
         block<MINMAX, 1>(a, acc, acc, i0, i_end);
     }
 
+    // exact mask test of the parked keys, then the survivors go in half by half
+    __device__ __forceinline__ void resolve_suspects(const ScoreArgs& a) {
+        if (!park) return;
+#if defined(LGX_MASK_ABL) && LGX_MASK_ABL == 3
+        return;
+#endif
+        const int n = user_ok ? *scnt() : 0;
+        if (__ballot(n > 0) == 0ull) return;
+        const uint64_t* susp = susp_slots(a);
+        uint32_t ok = 0;
+        for (int j = 0; j < n; ++j)
+            if (!is_masked(a, b, key_index(susp[j]))) ok |= 1u << j;
+        for (int ph = 0; ph < 2; ++ph) {
+            if (__ballot(ph == h && ok != 0u) == 0ull) continue;
+            if (ph == h) {
+                for (int j = 0; j < n; ++j)
+                    if ((ok >> j) & 1u) insert_key<false>(a, susp[j]);
+            }
+            sync_from(ph);
+        }
+        *scnt() = 0;
+        refresh_tau();
+    }
+
     __device__ __forceinline__ void flush(const ScoreArgs& a, int split, int lane) {
         drain(a);
+        resolve_suspects(a);
         if (user_ok && h == 0) {
             float* ps = a.part_score + ((size_t)b * a.n_splits + split) * k;
             int32_t* pi = a.part_idx + ((size_t)b * a.n_splits + split) * k;
@@ -738,6 +832,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
     }
     WaveTopK st;
     st.init(lk, lk + list_keys_per_wave(k), k, lane, b, user_ok);
+    st.enable_suspects(a);
     st.build_bloom(a);
     // consume the prologue loads here: otherwise the compiler treats them as possibly pending at
     // the loop header and waits vmcnt(0) -- i.e. for the tile prefetch -- in every iteration
@@ -748,7 +843,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
         uf[c] = __builtin_bit_cast(uint4, t);
     }
 #pragma unroll
-    for (int w = 0; w < 16; ++w) asm volatile("" : "+v"(st.bl[w]));
+    for (int w = 0; w < kBloomWords; ++w) asm volatile("" : "+v"(st.bl[w]));
 
     const int64_t i_begin = (int64_t)split * a.split_items;
     const int64_t i_end = min(a.n_items, i_begin + a.split_items);
@@ -934,7 +1029,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
     for (int64_t t = 0; t < ntiles; ++t) {
         LGX_STAT_T0
         const int64_t t0 = tile_start(t);
-        refill = ABLATE != 5 && t + ahead < ntiles;
+        refill = ABLATE != 5 && ABLATE != 7 && t + ahead < ntiles;
         if (refill) refill_t0 = tile_start(ABLATE == 6 ? 0 : t + ahead);  // 6 (development): L2-hot refills
         if (DMAPOS == 0 && refill) stage(sbuf, refill_t0);
 #ifdef LGX_SCORE_STATS
@@ -948,7 +1043,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
 #ifdef LGX_SCORE_STATS
         const uint64_t stat_t1_ = __builtin_amdgcn_s_memtime();
 #endif
-        if (ABLATE == 1 || ABLATE == 5 || ABLATE == 6) {  // development: MFMA + LDS pipeline only (5: no refills either) (keeps the accumulators live)
+        if (ABLATE == 1 || ABLATE == 5 || ABLATE == 6 || ABLATE == 7) {  // development: MFMA + LDS pipeline only (5: no refills either) (keeps the accumulators live)
             float z = 0.0f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) z += acc0[r] + (NACC == 2 ? acc1[r] : 0.0f);
@@ -972,8 +1067,10 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
         st.stat_[0] += 1;
 #endif
         // tiles t+2 .. t+ahead may stay in flight; tile t+1 must have landed
-        wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(t + ahead, ntiles - 1) - (t + 1)));
-        __syncthreads();
+        if (ABLATE != 7) {  // 7 (development): no refills and no barrier -- the MFMA + LDS-read ceiling
+            wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(t + ahead, ntiles - 1) - (t + 1)));
+            __syncthreads();
+        }
 #ifdef LGX_SCORE_STATS
         st.stat_[t < 1024 ? 12 : 6] += __builtin_amdgcn_s_memtime() - stat_t2_;  // wait + barrier
         st.stat_[t < 1024 ? 13 : 14] += 1;
@@ -1371,6 +1468,13 @@ struct UserRange {
     size_t ws_off;  // partial lists of this range inside the workspace
 };
 
+// workspace of one range: the split lists (scores, then indices), then the LDS kernel's parked keys
+size_t range_list_bytes(const UserRange& r, int k) { return align_up((size_t)(r.u1 - r.u0) * r.p.n_splits * k * 4); }
+size_t range_susp_bytes(const UserRange& r) {
+    return r.p.lds && r.p.n_splits == 1 ? align_up((size_t)(r.u1 - r.u0) * 2 * kSuspSlots * 8) : 0;
+}
+size_t range_ws_bytes(const UserRange& r, int k) { return 2 * range_list_bytes(r, k) + range_susp_bytes(r); }
+
 int plan_ranges(int64_t B, int64_t n_items, int dtype, int64_t d, int k, UserRange* r) {
     const SplitPlan p = plan_splits(B, n_items, dtype, d, k);
     int n = 0;
@@ -1386,7 +1490,7 @@ int plan_ranges(int64_t B, int64_t n_items, int dtype, int64_t d, int k, UserRan
     if (full < B) r[n++] = {full, B, plan_splits(B - full, n_items, dtype, d, k), 0};
     for (int i = 0; i < n; ++i) {
         r[i].ws_off = off;
-        off += align_up((size_t)(r[i].u1 - r[i].u0) * r[i].p.n_splits * k * 4) * 2;
+        off += range_ws_bytes(r[i], k);
     }
     return n;
 }
@@ -1395,7 +1499,7 @@ size_t topk_ws_bytes(int64_t B, int64_t n_items, int k, int dtype, int64_t d) {
     UserRange r[2];
     const int n = plan_ranges(B, n_items, dtype, d, k, r);
     size_t bytes = 0;
-    for (int i = 0; i < n; ++i) bytes += align_up((size_t)(r[i].u1 - r[i].u0) * r[i].p.n_splits * k * 4) * 2;
+    for (int i = 0; i < n; ++i) bytes += range_ws_bytes(r[i], k);
     return bytes + 512;  // + the global min / max words
 }
 
@@ -1476,12 +1580,13 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
         const UserRange& R = ranges[i];
         const SplitPlan& p = R.p;
         const int64_t Bi = R.u1 - R.u0;
-        const size_t list_bytes = align_up((size_t)Bi * p.n_splits * k * 4);
+        const size_t list_bytes = range_list_bytes(R, k);
         char* wsr = base + R.ws_off;
         const void* Qi = user_rows ? Q : static_cast<const void*>(static_cast<const char*>(Q) + R.u0 * d * esz);
         ScoreArgs a{Qi, user_rows ? user_rows + R.u0 : nullptr, items, Bi, n_items, d,
                     mask_indptr ? mask_indptr + R.u0 : nullptr, mask_indices, k, p.n_splits, p.split_items,
-                    reinterpret_cast<float*>(wsr), reinterpret_cast<int32_t*>(wsr + list_bytes), minmax};
+                    reinterpret_cast<float*>(wsr), reinterpret_cast<int32_t*>(wsr + list_bytes), minmax,
+                    range_susp_bytes(R) ? reinterpret_cast<uint64_t*>(wsr + 2 * list_bytes) : nullptr};
         int rc;
 #ifdef LGX_DEV_SWITCHES
         ScoreArgs ka = a;

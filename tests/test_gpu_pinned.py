@@ -126,6 +126,44 @@ def test_c5_scoring_full_sweep_plan_d256():
     assert torch.allclose(val[sel].double(), got, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("n_top,n_rand", [(10, 40), (40, 200)])
+def test_full_sweep_masks_on_the_top_items(n_top, n_rand):
+    """Full-sweep LDS kernel with every user's mask holding its own n_top best items plus n_rand
+    random ones: the masked items are exactly the candidates the sweep meets first-hand, and at
+    240 masked items the 256-bit Bloom filter passes nearly every survivor, so the parked-key slots
+    overflow into the immediate exact search.  Result: the exact top-k of the unmasked items."""
+    B, I, d, k = 256 * 256, 20_000, 256, 20
+    assert "full-sweep" in ops.score_topk_plan(B, I, d, torch.bfloat16, k)
+    g = torch.Generator(device=DEV).manual_seed(23)
+    Q = (torch.randn(B, d, device=DEV, generator=g) / 16).bfloat16()
+    items = (torch.randn(I, d, device=DEV, generator=g) / 16).bfloat16()
+    tops = []
+    for u0 in range(0, B, 8192):
+        s = Q[u0:u0 + 8192].float() @ items.float().T
+        tops.append(torch.topk(s, n_top, dim=1).indices)
+    top = torch.cat(tops)
+    m = torch.cat([top, torch.randint(0, I, (B, n_rand), device=DEV, generator=g)], 1).sort(1).values
+    keep = torch.ones_like(m, dtype=torch.bool)
+    keep[:, 1:] = m[:, 1:] != m[:, :-1]
+    indptr = torch.zeros(B + 1, dtype=torch.int64, device=DEV)
+    indptr[1:] = torch.cumsum(keep.sum(1), 0)
+    mask = (indptr, m[keep].to(torch.int32))
+    idx, val = lgx.score_topk(Q, items, k, mask=mask)
+    sel = torch.randint(0, B, (2000,), device=DEV, generator=g)
+    S = Q[sel].double() @ items.double().T
+    for j, u in enumerate(sel.tolist()):
+        S[j, mask[1][indptr[u]:indptr[u + 1]].long()] = float("-inf")
+    kth = torch.topk(S, k, dim=1).values[:, -1:]
+    got_idx = idx[sel].long()
+    assert (got_idx >= 0).all()
+    got = S.gather(1, got_idx)
+    assert torch.isfinite(got).all(), "a masked item was returned"
+    assert (got >= kth - 1e-5 * kth.abs().clamp(min=1.0)).all()
+    srt = got_idx.sort(1).values
+    assert (srt[:, 1:] != srt[:, :-1]).all()
+    assert torch.allclose(val[sel].double(), got, rtol=1e-5, atol=1e-5)
+
+
 def test_c1_gowalla_shape_vs_oracle():
     cfg = CONFIGS["gowalla"]
     u, i = synth_edges(cfg, 2020, DEV)

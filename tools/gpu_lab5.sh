@@ -1,0 +1,7 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 200 tools/score_lab 131072 > gpurun_out/lab5.txt 2>&1 || { cat gpurun_out/lab5.txt; exit 1; }
+LAB_NOSUSP=1 timeout -k 10 200 tools/score_lab 131072 >> gpurun_out/lab5.txt 2>&1 || { cat gpurun_out/lab5.txt; exit 1; }
+cat gpurun_out/lab5.txt
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_pinned.py tests/test_gpu_topk_eval.py -x -q --timeout 200 --timeout-method thread -k "score or topk or kat or Test or procedure or full_sweep" > gpurun_out/score_tests.txt 2>&1 || { tail -40 gpurun_out/score_tests.txt; exit 1; }
+tail -2 gpurun_out/score_tests.txt

@@ -39,7 +39,7 @@ int main(int argc, char** argv) {
     HK(hipMemcpy(mp, hp.data(), (B + 1) * 8, hipMemcpyHostToDevice));
     HK(hipMemcpy(mi, hi.data(), B * M * 4, hipMemcpyHostToDevice));
     const SplitPlan p = plan_splits(B, I, LGX_DTYPE_BF16, d, k);
-    HK(hipMalloc(&ws, (size_t)B * p.n_splits * k * 8 + 4096));
+    HK(hipMalloc(&ws, (size_t)B * p.n_splits * k * 8 + (size_t)B * p.n_splits * 2 * kSuspSlots * 8 + 4096));
     hipEvent_t e0, e1;
     HK(hipEventCreate(&e0));
     HK(hipEventCreate(&e1));
@@ -48,7 +48,8 @@ int main(int argc, char** argv) {
     auto timeit = [&](const char* name, auto fn, bool masked) -> int {
         ScoreArgs a{Q, nullptr, items, B, I, d, masked ? mp : nullptr, masked ? mi : nullptr, k, p.n_splits,
                     p.split_items, reinterpret_cast<float*>(ws),
-                    reinterpret_cast<int32_t*>(static_cast<char*>(ws) + (size_t)B * p.n_splits * k * 4), nullptr};
+                    reinterpret_cast<int32_t*>(static_cast<char*>(ws) + (size_t)B * p.n_splits * k * 4), nullptr,
+                    getenv("LAB_NOSUSP") ? nullptr : reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + (size_t)B * p.n_splits * k * 8)};
         if (fn(a, p, nullptr)) { std::printf("%s: launch failed: %s\n", name, lgx_last_error()); return 1; }
         float best = 1e30f;
         for (int r = 0; r < 3; ++r) {
@@ -64,14 +65,14 @@ int main(int argc, char** argv) {
         std::fflush(stdout);
         return 0;
     };
+#ifdef LGX_MASK_ABL
+    std::printf("LGX_MASK_ABL=%d\n", LGX_MASK_ABL);
+    if (timeit("full", launch<0, 0>, true)) return 1;
+#else
     for (int masked = 1; masked >= 0; --masked) {
-        if (timeit("full regroup-always", launch<0, 0, false>, masked)) return 1;
-        if (timeit("full fast-skip", launch<0, 0, true>, masked)) return 1;
+        if (timeit("full", launch<0, 0>, masked)) return 1;
     }
-    if (timeit("no-topk", launch<1, 0>, false)) return 1;
-    if (timeit("no-topk dma@kstep", launch<1, 1>, false)) return 1;
-    if (timeit("no-topk no-refill", launch<5, 0>, false)) return 1;
-    if (timeit("no-topk L2-hot refill", launch<6, 0>, false)) return 1;
+#endif
     std::printf("done\n");
     return 0;
 }
