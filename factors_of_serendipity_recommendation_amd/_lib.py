@@ -61,6 +61,10 @@ SIGNATURES = {
     "lgx_score_topk_plan": (_c_int, [_c_i64, _c_i64, _c_i64, _c_int, _c_int, ctypes.c_char_p, ctypes.c_size_t]),
     "lgx_strat_select_ex": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_int, _vp, ctypes.c_uint64, _vp, _c_int, _vp,
                                      _c_int, _vp]),
+    "lgx_strat_labels_fused": (_c_int, [_vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_float, _c_float, _c_int,
+                                        _vp, _vp, _vp, _vp, _vp]),
+    "lgx_strat_thresholds": (_c_int, [_c_float, _c_float, _c_int, _vp]),
+    "lgx_strat_hist": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _vp, _vp, _vp, _vp]),
     "lgx_parse_lines_workspace": (_c_int, [_c_i64, _sz_p]),
     "lgx_parse_lines_count": (_c_int, [_vp, _c_i64, _vp, ctypes.c_size_t, _vp, _vp]),
     "lgx_parse_lines_fill": (_c_int, [_vp, _c_i64, _vp, ctypes.c_size_t, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp]),

@@ -24,7 +24,9 @@
 //     the masked tail when fewer than k unmasked items exist, applies the optional sigmoid.
 #include <algorithm>
 #include <cmath>
+#include <cfloat>
 #include <cstdlib>
+#include <cstring>
 
 #include "wave_topk.h"
 
@@ -470,7 +472,6 @@ struct WaveTopK {
     // CHECK: test the mask here (drained keys were already filtered by drop_masked)
     template <bool CHECK>
     __device__ __forceinline__ void insert_key(const ScoreArgs& a, uint64_t key) {
-        const int32_t it = key_index(key);
         if (len == k) {
             if (key <= kmin || (CHECK && masked(a, key))) return;
             keys[mp] = key;
@@ -1300,6 +1301,169 @@ int kch_for(int dtype, int64_t d) {
     return -1;
 }
 
+// ---------------------------------------------------------------------------- stratification labels
+// f4 (recommend.py:375-381) fused: score_dense_lds's walk with the operands swapped (items are the
+// A operand, users the B operand -- the same k order, so the same f32 sums bit for bit), so that lane
+// (col, h) ends a tile holding 16 scores of ONE user (user u0 + col, items tile_row(r, h)): the
+// labels of items 8q + 4h + 0..3 pack into one dword store.  A label is the count of thresholds the
+// score reaches (lgx_strat_thresholds); nothing but the int8 labels leaves the chip.
+struct StratThr {
+    float t[32];
+    int n;
+    float base, inv;  // estimate: floor((s - base) * inv) is the label within +-1 (thresholds ~ evenly spaced)
+};
+
+// the label estimate of the kernel, on the host (same f32 operations, no contraction)
+inline int strat_estimate(float sc, const StratThr& thr) {
+    const float x = (sc - thr.base) * thr.inv;
+    return (x >= (float)thr.n || x != x) ? thr.n : (x < 0.0f ? 0 : (int)x);
+}
+inline int strat_label_host(float sc, const StratThr& thr) {
+    int l = 0;
+    for (int j = 0; j < thr.n; ++j) l += sc >= thr.t[j] ? 1 : 0;
+    return l;
+}
+// true when the estimate is within one of the label for every f32 score: both are monotone step
+// functions, so it suffices to look at both ends of every interval on which the estimate is
+// constant (found by bisection over the ordered f32 bit patterns)
+inline bool strat_estimate_within_one(const StratThr& thr) {
+    auto key = [](float f) {
+        int32_t b;
+        memcpy(&b, &f, 4);
+        return b >= 0 ? (int64_t)b : -(int64_t)(b & 0x7fffffff);
+    };
+    auto unkey = [](int64_t k) {
+        const int32_t b = k >= 0 ? (int32_t)k : (int32_t)((uint32_t)(-k) | 0x80000000u);
+        float f;
+        memcpy(&f, &b, 4);
+        return f;
+    };
+    const int64_t kmin = key(-FLT_MAX), kmax = key(FLT_MAX);
+    int64_t start = kmin;  // first f32 of the current estimate's interval
+    while (true) {
+        const int m = strat_estimate(unkey(start), thr);
+        // last f32 whose estimate is m
+        int64_t lo = start, hi = kmax;
+        while (lo < hi) {
+            const int64_t mid = lo + (hi - lo + 1) / 2;
+            if (strat_estimate(unkey(mid), thr) <= m) lo = mid;
+            else hi = mid - 1;
+        }
+        const int la = strat_label_host(unkey(start), thr), lb = strat_label_host(unkey(lo), thr);
+        if (la < m - 1 || lb > m + 1) return false;
+        if (lo >= kmax) return true;
+        start = lo + 1;
+    }
+}
+
+template <int DT, int KCH, bool VEC4, bool EST1>
+__global__ __launch_bounds__(kDenseWaves * 64) void strat_label_lds(const void* Q, const int64_t* user_rows,
+                                                                     const void* items, int64_t B, int64_t n_items,
+                                                                     int64_t d, StratThr thr,
+                                                                     int8_t* __restrict__ labels, int64_t n_ug,
+                                                                     int64_t split_items) {
+    static_assert(KCH >= 8, "swizzle needs >= 16 slots per row");
+    typedef Frag<DT> F;
+    constexpr int SPR = 2 * KCH;
+    constexpr int RB = SPR * 16;
+    constexpr int TILE = 32 * RB;
+    constexpr int NL = 32 * SPR / (kDenseWaves * 64);
+    static_assert(NL >= 1 && 32 * SPR % (kDenseWaves * 64) == 0, "tile slots must divide over the workgroup");
+    __shared__ __attribute__((aligned(16))) unsigned char img[2][TILE];
+    // T[j] = the score where label j starts (T[0] = -inf, T[n + 1] = +inf): the label of s is the
+    // estimate e corrected by one compare on each side, s < T[e] and s >= T[e + 1]
+    __shared__ float T[34];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int h = lane >> 5, col = lane & 31;
+    if (threadIdx.x < 34)
+        T[threadIdx.x] = threadIdx.x == 0 ? -INFINITY : (threadIdx.x <= thr.n ? thr.t[threadIdx.x - 1] : INFINITY);
+    const int64_t L = blockIdx.x, kk = L >> 3;
+    const int64_t ug = kk % n_ug;
+    const int64_t split = (kk / n_ug) * 8 + (L & 7);
+    const int64_t u0 = ug * kDenseUsers + (int64_t)wave * kUsersPerWave;
+    const bool wave_on = u0 < B;
+    const int64_t b = u0 + col;
+    const bool user_ok = b < B;
+    const int64_t qrow = user_ok ? (user_rows ? user_rows[b] : b) : 0;
+    typename F::chunk uf[KCH];
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) uf[c] = F::load(Q, qrow, d, c, h, user_ok);
+    const int64_t i_begin = split * split_items;
+    const int64_t i_end = std::min(n_items, i_begin + split_items);
+    const int64_t row_bytes = d * (DT == LGX_DTYPE_F32 ? 4 : 2);
+    const unsigned char* ib = static_cast<const unsigned char*>(items);
+    int8_t* lab = labels + b * n_items;
+    uint4 nx[NL];
+    auto load_tile = [&](int64_t i0) {
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int sl = threadIdx.x + j * kDenseWaves * 64;
+            const int r = sl / SPR, q = sl % SPR;
+            const int64_t it = i0 + r;
+            nx[j] = (it < i_end && q * 16 < row_bytes)
+                        ? *reinterpret_cast<const uint4*>(ib + it * row_bytes + q * 16)
+                        : make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
+    auto store_tile = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int sl = threadIdx.x + j * kDenseWaves * 64;
+            const int r = sl / SPR, q = sl % SPR;
+            *reinterpret_cast<uint4*>(&img[buf][r * RB + ((q ^ (r & 15)) * 16)]) = nx[j];
+        }
+    };
+    auto label = [&](float sc) {
+        const float x = (sc - thr.base) * thr.inv;
+        int l = (x >= (float)thr.n || x != x) ? thr.n : (x < 0.0f ? 0 : (int)x);  // NaN -> n, as label_of
+        if (EST1) {  // the host proved |estimate - label| <= 1: one branch-free step each way
+            const int lo = l, up = l < thr.n ? l + 1 : l;
+            return (uint32_t)(l - (sc < T[lo] && l > 0 ? 1 : 0) + (sc >= T[up] && l < thr.n ? 1 : 0));
+        }
+        while (l > 0 && sc < T[l]) --l;  // exact whatever the estimate
+        while (l < thr.n && sc >= T[l + 1]) ++l;
+        return (uint32_t)l;
+    };
+    if (i_begin >= i_end) return;  // workgroup-uniform
+    load_tile(i_begin);
+    store_tile(0);
+    __syncthreads();
+    int buf = 0;
+    for (int64_t i0 = i_begin; i0 < i_end; i0 += 32) {
+        const bool more = i0 + 32 < i_end;  // workgroup-uniform
+        if (more) load_tile(i0 + 32);
+        if (wave_on) {
+            const unsigned char* rowp = &img[buf][col * RB];
+            f32x16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+            for (int c = 0; c < KCH; ++c) {
+                const uint4 fr = *reinterpret_cast<const uint4*>(rowp + (((2 * c + h) ^ (col & 15)) * 16));
+                acc = F::mma(__builtin_bit_cast(typename F::chunk, fr), uf[c], acc);
+            }
+            if (user_ok) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int64_t it = i0 + 8 * q + 4 * h;  // items it .. it + 3: acc rows 4q .. 4q + 3
+                    const uint32_t w = label(acc[4 * q]) | (label(acc[4 * q + 1]) << 8) |
+                                       (label(acc[4 * q + 2]) << 16) | (label(acc[4 * q + 3]) << 24);
+                    if (VEC4 && it + 4 <= i_end) {
+                        *reinterpret_cast<uint32_t*>(lab + it) = w;
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (it + e < i_end) lab[it + e] = (int8_t)((w >> (8 * e)) & 255);
+                    }
+                }
+            }
+        }
+        if (more) store_tile(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+}
+
 struct SplitPlan {
     int n_splits;
     int64_t split_items;
@@ -1656,4 +1820,59 @@ extern "C" int lgx_score_dense(const void* Q, const int64_t* user_rows, const vo
 #undef LGX_SD
     LGX_LAUNCH_CHECK();
     return LGX_OK;
+}
+
+extern "C" int lgx_strat_labels_fused(const void* Q, const int64_t* user_rows, const void* items, int64_t B,
+                                      int64_t n_items, int64_t d, int dtype, float min16, float inter16,
+                                      int num_fold, const int64_t* mask_indptr, const int32_t* mask_indices,
+                                      int8_t* labels, int32_t* hist, lgx_stream_t stream_) {
+    hipStream_t stream = as_hip(stream_);
+    LGX_REQUIRE(B >= 0 && n_items >= 0 && n_items < INT32_MAX && (B == 0 || (Q && items && labels && hist)),
+                LGX_ERR_INVALID_ARG, "lgx_strat_labels_fused: bad arguments");
+    LGX_REQUIRE(dtype == LGX_DTYPE_F32 || dtype == LGX_DTYPE_BF16, LGX_ERR_INVALID_ARG,
+                "lgx_strat_labels_fused: dtype");
+    const int64_t vec = dtype == LGX_DTYPE_F32 ? 4 : 8;
+    const int kch = kch_for(dtype, d);
+    LGX_REQUIRE(d > 0 && d % vec == 0 && kch >= 8, LGX_ERR_UNSUPPORTED,
+                "lgx_strat_labels_fused: d=%lld: a multiple of %lld with 5..32 MFMA chunks (use lgx_score_dense + "
+                "lgx_strat_labels)", (long long)d, (long long)vec);
+    StratThr thr{};
+    LGX_REQUIRE(num_fold >= 1 && num_fold < 32, LGX_ERR_INVALID_ARG, "lgx_strat_labels_fused: num_fold in [1, 32)");
+    int rc = lgx_strat_thresholds(min16, inter16, num_fold, thr.t);
+    if (rc) return rc;
+    thr.n = num_fold;
+    // the estimate's grid: label j starts near thr[j-1]; evenly spaced by the mean gap
+    thr.base = thr.t[0] - (num_fold > 1 && std::isfinite(thr.t[num_fold - 1])
+                               ? (thr.t[num_fold - 1] - thr.t[0]) / (num_fold - 1) : inter16);
+    thr.inv = num_fold > 1 && std::isfinite(thr.t[num_fold - 1]) && thr.t[num_fold - 1] > thr.t[0]
+                  ? (float)(num_fold - 1) / (thr.t[num_fold - 1] - thr.t[0]) : 1.0f / inter16;
+    if (B == 0 || n_items == 0) return LGX_OK;
+    const int64_t n_ug = ceil_div(B, (int64_t)kDenseUsers);
+    const int64_t tiles = ceil_div(n_items, 32);
+    const int64_t n_splits = std::max<int64_t>(8, std::min(8 * ceil_div(ceil_div(2048, n_ug), 8), 8 * ceil_div(tiles, 8)));
+    const int64_t split_items = 32 * ceil_div(tiles, n_splits);
+    const int64_t grid = n_ug * n_splits;
+    LGX_REQUIRE(grid < (1LL << 31), LGX_ERR_UNSUPPORTED, "lgx_strat_labels_fused: %lld users is too many", (long long)B);
+    const bool vec4 = n_items % 4 == 0 && ((uintptr_t)labels & 3) == 0;
+    const bool est1 = strat_estimate_within_one(thr);
+#define LGX_SL3(DTV, KC, V4)                                                                                      \
+    if (est1)                                                                                                     \
+        strat_label_lds<DTV, KC, V4, true><<<(unsigned)grid, kDenseWaves * 64, 0, stream>>>(                      \
+            Q, user_rows, items, B, n_items, d, thr, labels, n_ug, split_items);                                  \
+    else                                                                                                          \
+        strat_label_lds<DTV, KC, V4, false><<<(unsigned)grid, kDenseWaves * 64, 0, stream>>>(                     \
+            Q, user_rows, items, B, n_items, d, thr, labels, n_ug, split_items)
+#define LGX_SL2(DTV, KC, V4) do { LGX_SL3(DTV, KC, V4); } while (0)
+#define LGX_SL_ALL(DTV)                                                              \
+    switch (kch) {                                                                   \
+        case 8: if (vec4) LGX_SL2(DTV, 8, true); else LGX_SL2(DTV, 8, false); break;    \
+        case 16: if (vec4) LGX_SL2(DTV, 16, true); else LGX_SL2(DTV, 16, false); break; \
+        default: if (vec4) LGX_SL2(DTV, 32, true); else LGX_SL2(DTV, 32, false); break; \
+    }
+    if (dtype == LGX_DTYPE_F32) { LGX_SL_ALL(LGX_DTYPE_F32) } else { LGX_SL_ALL(LGX_DTYPE_BF16) }
+#undef LGX_SL_ALL
+#undef LGX_SL2
+#undef LGX_SL3
+    LGX_LAUNCH_CHECK();
+    return lgx_strat_hist(labels, B, n_items, num_fold, mask_indptr, mask_indices, hist, stream_);
 }

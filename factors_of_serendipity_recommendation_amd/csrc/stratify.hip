@@ -22,22 +22,26 @@
 
 #include <hip/hip_fp16.h>
 
+#include <cfloat>
+#include <cstring>
+
 namespace lgx {
 namespace {
 
 constexpr int kStratThreads = 256;
 constexpr int kMaxFolds = 32;
 constexpr int kMaxStratK = 1024;  // candidates per user that the selection kernel keeps in LDS
-constexpr int kMaxCand = 2048;    // fast-path candidates (13 B each) in the radix histogram's 32 KB
+constexpr int kMaxCand = 2048;    // fast-path candidates (12 B each) in the radix histogram's 32 KB
 
-__device__ __forceinline__ float half_round(float x) { return __half2float(__float2half_rn(x)); }
+__host__ __device__ __forceinline__ float half_round(float x) { return __half2float(__float2half_rn(x)); }
 
-__device__ __forceinline__ int label_of(float sc, float min16, float inter16, int num_fold) {
+__host__ __device__ __forceinline__ int label_of(float sc, float min16, float inter16, int num_fold) {
     // numpy float16: every operation in float, rounded back to half
     const float d = half_round(half_round(sc) - min16);
     const float q = half_round(d / inter16);
-    const int lv = (int)floorf(q);
-    return lv < 0 ? 0 : (lv > num_fold ? num_fold : lv);  // d >= 0; the top bin is label num_fold
+    if (!(q < (float)num_fold)) return num_fold;  // the top bin is label num_fold (also q = +inf)
+    if (q < 0.0f) return 0;                       // scores below min_dis (d >= 0 for real rows)
+    return (int)floorf(q);
 }
 
 // Labels of every item first (4 per thread and float4 / 32-bit accesses when rows are 16-B
@@ -113,20 +117,99 @@ __global__ __launch_bounds__(kStratThreads) void strat_labels_kernel(const float
     if (threadIdx.x <= num_fold) hist[u * (num_fold + 1) + threadIdx.x] = h[threadIdx.x];
 }
 
+// Counts of an int8 label row (per-thread LDS counters, summed per bin), then the masked items
+// relabelled -1 and taken out: the tail of strat_labels_kernel for rows the fused scoring kernel
+// (lgx_strat_labels_fused) labelled.  16 labels per 16-B load when the rows allow it.
+template <bool VEC16>
+__global__ __launch_bounds__(kStratThreads) void strat_hist_kernel(int8_t* __restrict__ labels, int64_t n_items,
+                                                                  int num_fold, const int64_t* __restrict__ mask_indptr,
+                                                                  const int32_t* __restrict__ mask_indices,
+                                                                  int32_t* __restrict__ hist) {
+    __shared__ uint32_t hp[kMaxFolds * kStratThreads];
+    __shared__ int32_t h[kMaxFolds];
+    const int64_t u = blockIdx.x;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int b = 0; b < kMaxFolds; ++b) hp[b * kStratThreads + tid] = 0;
+    __syncthreads();
+    int8_t* lab = labels + u * n_items;
+    if (VEC16) {
+        const int64_t n16 = n_items >> 4;
+        for (int64_t q = tid; q < n16; q += kStratThreads) {
+            const uint4 w = reinterpret_cast<const uint4*>(lab)[q];
+            const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int j = 0; j < 16; ++j) hp[((ws[j >> 2] >> (8 * (j & 3))) & 255) * kStratThreads + tid] += 1;
+        }
+    } else {
+        for (int64_t i = tid; i < n_items; i += kStratThreads) hp[(uint8_t)lab[i] * kStratThreads + tid] += 1;
+    }
+    __syncthreads();
+    if (tid < kMaxFolds) {
+        uint32_t c = 0;
+        for (int t = 0; t < kStratThreads; ++t) c += hp[tid * kStratThreads + ((t + tid) & (kStratThreads - 1))];
+        h[tid] = (int32_t)c;
+    }
+    __syncthreads();
+    if (mask_indptr) {
+        const int64_t m0 = mask_indptr[u], m1 = mask_indptr[u + 1];
+        for (int64_t j = m0 + threadIdx.x; j < m1; j += kStratThreads) {
+            const int32_t it = mask_indices[j];
+            if (it < 0 || it >= n_items || (j > m0 && mask_indices[j - 1] == it)) continue;  // sorted: skip repeats
+            atomicSub(&h[lab[it]], 1);
+            lab[it] = -1;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x <= num_fold) hist[u * (num_fold + 1) + threadIdx.x] = h[threadIdx.x];
+}
+
 // per-user random order of the items: high word = a 32-bit bijection of the item index (odd
 // multiply, xor with the user's seed word, murmur3 fmix32), low word = the index -- distinct keys,
 // ~7 32-bit ops per item instead of two 64-bit splitmix rounds (the select's dominant cost)
 __device__ __forceinline__ uint32_t user_seed_word(uint64_t seed, int64_t u) {
     return (uint32_t)(splitmix64(seed ^ splitmix64((uint64_t)u ^ 0xA5A5A5A5ull)) >> 32);
 }
-__device__ __forceinline__ uint64_t item_key(uint32_t us, int64_t i) {
+__device__ __forceinline__ uint32_t item_hash(uint32_t us, int64_t i) {
     uint32_t x = ((uint32_t)i * 0x9E3779B1u) ^ us;
     x ^= x >> 16;
     x *= 0x85EBCA6Bu;
     x ^= x >> 13;
     x *= 0xC2B2AE35u;
     x ^= x >> 16;
-    return ((uint64_t)x << 32) | (uint32_t)i;
+    return x;
+}
+__device__ __forceinline__ uint64_t item_key(uint32_t us, int64_t i) {
+    return ((uint64_t)item_hash(us, i) << 32) | (uint32_t)i;
+}
+
+// Ascending bitonic sort of n (a power of two) (key, value) pairs in LDS by the whole workgroup;
+// the caller pads with ~0 keys.  O(n log^2 n / threads) with one barrier per stage, instead of the
+// O(n^2 / threads) rank loop whose LDS reads each waited on the one before.
+__device__ __forceinline__ void lds_bitonic(uint64_t* k, int32_t* v, int n) {
+    for (int size = 2; size <= n; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            __syncthreads();
+            for (int t = threadIdx.x; t < n / 2; t += kStratThreads) {
+                const int i = 2 * t - (t & (stride - 1)), j = i + stride;
+                const uint64_t a = k[i], b = k[j];
+                if ((a > b) == ((i & size) == 0)) {
+                    k[i] = b;
+                    k[j] = a;
+                    const int32_t x = v[i];
+                    v[i] = v[j];
+                    v[j] = x;
+                }
+            }
+        }
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ int pow2_at_least(int n) {
+    int p = 1;
+    while (p < n) p <<= 1;
+    return p;
 }
 
 // np.rint: round half to even
@@ -149,6 +232,10 @@ __global__ __launch_bounds__(kStratThreads) void strat_select_kernel(const int8_
     __shared__ uint64_t keys_sh[kMaxStratK];
     __shared__ int32_t items_sh[kMaxStratK];
     __shared__ int32_t n_sel;
+    // high word of cut[l] by the label's byte (0 for labels with nothing to take and for -1 = 255):
+    // the per-item test is one hash and one compare against it; the full key test runs only for
+    // the few items at or under it
+    __shared__ uint32_t cut_hi[256];
     const int64_t u = blockIdx.x;
     const int tid = threadIdx.x;
     const uint32_t us = user_seed_word(seed, u);
@@ -173,7 +260,6 @@ __global__ __launch_bounds__(kStratThreads) void strat_select_kernel(const int8_
     // runs only when a label came up short or the buffer overflowed.
     uint64_t* ck = reinterpret_cast<uint64_t*>(dh);
     int32_t* ci = reinterpret_cast<int32_t*>(ck + kMaxCand);
-    int8_t* cl = reinterpret_cast<int8_t*>(ci + kMaxCand);
     if (tid < n_bins) {
         const int64_t hl = hist[u * n_bins + tid], nl = need[tid];
         const double frac = hl > 0 ? ((double)nl + 4.0 * sqrt((double)nl) + 8.0) / (double)hl : 2.0;
@@ -182,25 +268,38 @@ __global__ __launch_bounds__(kStratThreads) void strat_select_kernel(const int8_
     }
     if (tid == 0) n_cand = 0;
     __syncthreads();
+    cut_hi[tid] = (tid < n_bins && need[tid] > 0) ? (uint32_t)(cut[tid] >> 32) : 0u;
+    __syncthreads();
+    // a candidate's sort key: label above the hash (the hash is a bijection of the item index, so
+    // ordering by it orders by the full (hash, item) key)
     auto consider = [&](int64_t i, int l) {
+        const uint32_t x = item_hash(us, i);
+        if (x > cut_hi[l & 255]) return;  // most items stop here
         if (l < 0 || l >= n_bins || need[l] <= 0) return;
-        const uint64_t k = item_key(us, i);
-        if (k > cut[l]) return;
+        if (item_key(us, i) > cut[l]) return;
         atomicAdd(&cand_l[l], 1);
         const int slot = atomicAdd(&n_cand, 1);
         if (slot < kMaxCand) {
-            ck[slot] = k;
+            ck[slot] = ((uint64_t)l << 32) | x;
             ci[slot] = (int32_t)i;
-            cl[slot] = (int8_t)l;
         }
     };
-    if (VEC16) {  // 16 labels per 16-B load
+    if (VEC16) {  // 16 labels per 16-B load; the 16 table lookups issue together, then the rare hits
         const int64_t n16 = n_items >> 4;
         for (int64_t q = tid; q < n16; q += kStratThreads) {
             const uint4 w = reinterpret_cast<const uint4*>(lab)[q];
             const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+            uint32_t hit = 0;
 #pragma unroll
-            for (int j = 0; j < 16; ++j) consider(16 * q + j, (int)(int8_t)(ws[j >> 2] >> (8 * (j & 3))));
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t lb = (ws[j >> 2] >> (8 * (j & 3))) & 255u;
+                hit |= (item_hash(us, 16 * q + j) <= cut_hi[lb] ? 1u : 0u) << j;
+            }
+            while (hit) {
+                const int j = __builtin_ctz(hit);
+                hit &= hit - 1;
+                consider(16 * q + j, (int)(int8_t)(ws[j >> 2] >> (8 * (j & 3))));
+            }
         }
     } else {
         for (int64_t i = tid; i < n_items; i += kStratThreads) consider(i, lab[i]);
@@ -213,20 +312,29 @@ __global__ __launch_bounds__(kStratThreads) void strat_select_kernel(const int8_
     }
     __syncthreads();
     if (fast_ok) {
-        // rank of each candidate inside its label by (key, item); the need[l] lowest are taken
-        const int m = n_cand;
+        // sort the candidates by (label, hash): label l's run starts at the count of the labels
+        // below it, and its first need[l] entries are its picks (placed at fixed slots, no atomics)
+        const int m = n_cand, P = pow2_at_least(m);
+        for (int a = m + tid; a < P; a += kStratThreads) ck[a] = ~0ull;
+        lds_bitonic(ck, ci, P);
+        __shared__ int32_t run0[kMaxFolds], pick0[kMaxFolds];
+        if (tid == 0) {
+            int r = 0, q = 0;
+            for (int l = 0; l < n_bins; ++l) {
+                run0[l] = r;
+                pick0[l] = q;
+                r += cand_l[l];
+                q += need[l] > 0 ? (int)need[l] : 0;
+            }
+            n_sel = q;
+        }
+        __syncthreads();
         for (int a = tid; a < m; a += kStratThreads) {
-            const uint64_t ka = ck[a];
-            const int la = cl[a], ia = ci[a];
-            int r = 0;
-            for (int b2 = 0; b2 < m; ++b2)
-                r += (cl[b2] == la && (ck[b2] < ka || (ck[b2] == ka && ci[b2] < ia))) ? 1 : 0;
-            if (r < need[la]) {
-                const int slot = atomicAdd(&n_sel, 1);
-                if (slot < kMaxStratK) {
-                    keys_sh[slot] = ka;
-                    items_sh[slot] = ia;
-                }
+            const int l = (int)(ck[a] >> 32), r = a - run0[l];
+            const int slot = pick0[l] + r;
+            if (r < need[l] && slot < kMaxStratK) {
+                keys_sh[slot] = ((ck[a] & 0xffffffffull) << 32) | (uint32_t)ci[a];
+                items_sh[slot] = ci[a];
             }
         }
         __syncthreads();
@@ -282,18 +390,13 @@ __global__ __launch_bounds__(kStratThreads) void strat_select_kernel(const int8_
     }
     __syncthreads();
     const int n = min(n_sel, kMaxStratK);
-    // order by key: rank of each pick among all picks (n <= 1024, O(n^2 / threads))
-    __shared__ int32_t ranked[kMaxStratK];
-    for (int a = tid; a < n; a += kStratThreads) {
-        int r = 0;
-        const uint64_t ka = keys_sh[a];
-        for (int b = 0; b < n; ++b) {
-            const uint64_t kb = keys_sh[b];
-            r += (kb < ka || (kb == ka && items_sh[b] < items_sh[a])) ? 1 : 0;
-        }
-        ranked[r] = items_sh[a];
+    // order the picks by key (keys are distinct): a random order fixed by the seed
+    {
+        const int P = pow2_at_least(n);
+        for (int a = n + tid; a < P; a += kStratThreads) keys_sh[a] = ~0ull;
+        lds_bitonic(keys_sh, items_sh, P);
     }
-    __syncthreads();
+    const int32_t* ranked = items_sh;
     // sample_list (recommend.py:314-325): trim to K, or pad with distinct draws from the list
     const int K = target;
     int32_t* o = out + u * (int64_t)out_stride;
@@ -324,6 +427,59 @@ extern "C" int lgx_strat_labels(const float* scores, int64_t n_users, int64_t n_
         strat_labels_kernel<false><<<(unsigned)n_users, kStratThreads, 0, as_hip(stream)>>>(
             scores, n_items, min16, inter16, num_fold, mask_indptr, mask_indices, labels, hist);
     LGX_LAUNCH_CHECK();
+    return LGX_OK;
+}
+
+extern "C" int lgx_strat_hist(int8_t* labels, int64_t n_users, int64_t n_items, int num_fold,
+                              const int64_t* mask_indptr, const int32_t* mask_indices, int32_t* hist,
+                              lgx_stream_t stream) {
+    LGX_REQUIRE(n_users >= 0 && n_items >= 0 && num_fold >= 1 && num_fold < kMaxFolds && n_items < INT32_MAX,
+                LGX_ERR_INVALID_ARG, "lgx_strat_hist: bad sizes (num_fold in [1, %d))", kMaxFolds);
+    if (n_users == 0) return LGX_OK;
+    LGX_REQUIRE(labels && hist && (!mask_indptr || mask_indices), LGX_ERR_INVALID_ARG, "lgx_strat_hist: null pointer");
+    const bool vec16 = n_items % 16 == 0 && ((uintptr_t)labels & 15) == 0;
+    if (vec16)
+        strat_hist_kernel<true><<<(unsigned)n_users, kStratThreads, 0, as_hip(stream)>>>(
+            labels, n_items, num_fold, mask_indptr, mask_indices, hist);
+    else
+        strat_hist_kernel<false><<<(unsigned)n_users, kStratThreads, 0, as_hip(stream)>>>(
+            labels, n_items, num_fold, mask_indptr, mask_indices, hist);
+    LGX_LAUNCH_CHECK();
+    return LGX_OK;
+}
+
+// The label of a score is a monotone step function of it (each float16 rounding, the subtraction,
+// the division by inter16 > 0 and the floor are monotone), so thr[j-1] = the smallest f32 x with
+// label_of(x) >= j, found by bisection over the ordered f32 bit patterns, gives
+// label_of(s) = #{j : s >= thr[j-1]} for every finite s.
+extern "C" int lgx_strat_thresholds(float min16, float inter16, int num_fold, float* thr) {
+    LGX_REQUIRE(thr && num_fold >= 1 && num_fold < kMaxFolds && inter16 > 0.0f, LGX_ERR_INVALID_ARG,
+                "lgx_strat_thresholds: bad arguments");
+    auto key = [](float f) {  // order-preserving f32 -> int64
+        int32_t b;
+        memcpy(&b, &f, 4);
+        return b >= 0 ? (int64_t)b : -(int64_t)(b & 0x7fffffff);
+    };
+    auto unkey = [](int64_t k) {
+        const int32_t b = k >= 0 ? (int32_t)k : (int32_t)((uint32_t)(-k) | 0x80000000u);
+        float f;
+        memcpy(&f, &b, 4);
+        return f;
+    };
+    const int64_t kmin = key(-FLT_MAX), kmax = key(FLT_MAX);
+    for (int j = 1; j <= num_fold; ++j) {
+        int64_t lo = kmin, hi = kmax;  // invariant: label(unkey(hi)) >= j, or hi == kmax
+        if (label_of(unkey(hi), min16, inter16, num_fold) < j) {
+            thr[j - 1] = INFINITY;  // no finite score reaches label j
+            continue;
+        }
+        while (lo < hi) {
+            const int64_t mid = lo + (hi - lo) / 2;
+            if (label_of(unkey(mid), min16, inter16, num_fold) >= j) hi = mid;
+            else lo = mid + 1;
+        }
+        thr[j - 1] = unkey(lo);
+    }
     return LGX_OK;
 }
 

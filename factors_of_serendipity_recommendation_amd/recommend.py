@@ -19,7 +19,7 @@ may produce.
 from __future__ import annotations
 
 import os
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -167,12 +167,47 @@ def stratification_bounds(emb_user: torch.Tensor, emb_item: torch.Tensor, num_fo
     return float(min_dis), float(inter)
 
 
+def fused_labels_eligible(emb_user: torch.Tensor, d: int) -> bool:
+    """lgx_strat_labels_fused covers 5..32 MFMA chunks per row (f32 d 40..256, bf16 d 80..256)."""
+    per = 8 if emb_user.dtype == torch.float32 else 16
+    return emb_user.dtype in (torch.float32, torch.bfloat16) and d % (per // 2) == 0 and 4 * per < d <= 256
+
+
+def strat_labels(emb_user: torch.Tensor, emb_item: torch.Tensor, mask_indptr: torch.Tensor,
+                 mask_indices: torch.Tensor, min16: float, inter16: float, num_fold: int,
+                 fused: Optional[bool] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Labels [U, I] int8 and label counts [U, num_fold + 1] of recommend.py:375-381 for a batch of
+    users: fused (the MFMA epilogue labels the scores; no [U, I] f32 matrix) when the shape allows,
+    else lgx_score_dense rows + lgx_strat_labels.  Both give the same bits."""
+    from . import _lib
+    dev = emb_user.device
+    U, I = emb_user.shape[0], emb_item.shape[0]
+    L = _lib.lib()
+    st = ops._stream_ptr(dev)
+    labels = torch.empty((U, I), dtype=torch.int8, device=dev)
+    hist = torch.empty((U, num_fold + 1), dtype=torch.int32, device=dev)
+    if fused is None:
+        fused = fused_labels_eligible(emb_user, emb_user.shape[1])
+    if fused:
+        Q, it = emb_user.contiguous(), emb_item.contiguous()
+        _lib.check(L.lgx_strat_labels_fused(Q.data_ptr(), None, it.data_ptr(), U, I, Q.shape[1], ops._dtype_code(Q),
+                                            min16, inter16, num_fold, mask_indptr.data_ptr(), mask_indices.data_ptr(),
+                                            labels.data_ptr(), hist.data_ptr(), st), "lgx_strat_labels_fused")
+    else:
+        S = ops.score_dense(emb_user.contiguous(), emb_item)
+        _lib.check(L.lgx_strat_labels(S.data_ptr(), U, I, min16, inter16, num_fold, mask_indptr.data_ptr(),
+                                      mask_indices.data_ptr(), labels.data_ptr(), hist.data_ptr(), st),
+                   "lgx_strat_labels")
+        del S
+    return labels, hist
+
+
 def stratified_candidates(emb_user: torch.Tensor, emb_item: torch.Tensor, train: Sequence[Sequence[int]],
                           targets: Sequence[int], num_fold: int = 10, epsilon: float = 0.1, seed: int = 0,
-                          batch: int = 4096) -> List[List[int]]:
+                          batch: int = 4096, fused: Optional[bool] = None) -> List[List[int]]:
     """Per user, the stratified candidate list of create_candidates_stratification_sub +
-    sample_list (recommend.py:314-356): labels by lgx_strat_labels over lgx_score_dense rows, the
-    per-label random picks by lgx_strat_select."""
+    sample_list (recommend.py:314-356): labels and counts by strat_labels (fused into the scoring
+    kernel's epilogue where the shape allows), the per-label random picks by lgx_strat_select."""
     from . import _lib
     dev = emb_user.device
     U, I = emb_user.shape[0], emb_item.shape[0]
@@ -185,12 +220,7 @@ def stratified_candidates(emb_user: torch.Tensor, emb_item: torch.Tensor, train:
     st = ops._stream_ptr(dev)
     for b0 in range(0, U, batch):
         b1 = min(U, b0 + batch)
-        S = ops.score_dense(emb_user[b0:b1].contiguous(), emb_item)
-        labels = torch.empty((b1 - b0, I), dtype=torch.int8, device=dev)
-        hist = torch.empty((b1 - b0, num_fold + 1), dtype=torch.int32, device=dev)
-        _lib.check(L.lgx_strat_labels(S.data_ptr(), b1 - b0, I, min16, inter16, num_fold, mp[b0:].data_ptr(),
-                                      mi.data_ptr(), labels.data_ptr(), hist.data_ptr(), st), "lgx_strat_labels")
-        del S
+        labels, hist = strat_labels(emb_user[b0:b1], emb_item, mp[b0:], mi, min16, inter16, num_fold, fused)
         out = torch.empty((b1 - b0, K), dtype=torch.int32, device=dev)
         cnt = torch.empty(b1 - b0, dtype=torch.int32, device=dev)
         _lib.check(L.lgx_strat_select(labels.data_ptr(), b1 - b0, I, hist.data_ptr(), num_fold + 1,

@@ -230,6 +230,24 @@ int lgx_strat_select(const int8_t* labels, int64_t n_users, int64_t n_items, con
 int lgx_strat_select_ex(const int8_t* labels, int64_t n_users, int64_t n_items, const int32_t* hist, int n_bins,
                         const int32_t* targets, uint64_t seed, int32_t* out, int out_stride, int32_t* out_count,
                         int flags, lgx_stream_t stream);
+/*
+ * Fused form of lgx_score_dense + lgx_strat_labels (recommend.py:375-381): the user x item dots on
+ * the matrix cores, labelled in the MFMA epilogue -- the [U, I] f32 score matrix is never written.
+ * Labels and hist are bit-identical to the two-step path (same MFMA accumulation order; the float16
+ * label arithmetic is a monotone step function of the f32 score, so it is evaluated as a count of
+ * thresholds from lgx_strat_thresholds).  Q [n_users, d] (or the rows user_rows), items [n_items, d],
+ * f32 or bf16; d / (8 f32 | 16 bf16) in 5..32 chunks (f32 d 40..256, bf16 d 80..256).
+ */
+int lgx_strat_labels_fused(const void* Q, const int64_t* user_rows, const void* items, int64_t n_users,
+                           int64_t n_items, int64_t d, int dtype, float min16, float inter16, int num_fold,
+                           const int64_t* mask_indptr, const int32_t* mask_indices, int8_t* labels,
+                           int32_t* hist, lgx_stream_t stream);
+/* host only: thr[j-1] = the smallest f32 score whose label is >= j, j = 1..num_fold (num_fold < 32) */
+int lgx_strat_thresholds(float min16, float inter16, int num_fold, float* thr);
+/* label counts of rows of an int8 label matrix, then the user's masked items relabelled -1 and taken
+ * out of the counts (the last step of lgx_strat_labels, for labels written by the fused kernel) */
+int lgx_strat_hist(int8_t* labels, int64_t n_users, int64_t n_items, int num_fold, const int64_t* mask_indptr,
+                   const int32_t* mask_indices, int32_t* hist, lgx_stream_t stream);
 
 /* ---------------------------------------------------------------- 8(f) rank 3: interaction files */
 /*

@@ -92,3 +92,30 @@ def test_stratification_rejects_bad_arguments_before_device_work():
     assert L.lgx_strat_labels(p, 1, 10, 0.0, 0.0, 10, None, None, p, p, None) == 1  # inter must be > 0
     assert L.lgx_strat_labels(p, 1, 10, 0.0, 0.5, 40, None, None, p, p, None) == 1  # too many folds
     assert L.lgx_strat_select(p, 1, 10, p, 11, p, 1, p, 2048, p, None) == 3         # > 1024 per user
+
+
+@pytest.mark.parametrize("mn,mx,num_fold", [(-0.731, 1.42, 10), (0.0, 3.0, 10), (-4.5, 2.25, 7), (-1e-3, 1e-3, 10),
+                                            (-20.0, 35.5, 31)])
+def test_strat_thresholds_reproduce_float16_labels(mn, mx, num_fold):
+    """Host only: lgx_strat_thresholds' step function == numpy's float16 label arithmetic
+    (recommend.py:375-381: (f16(s) - min16) / inter16, floored, every operation rounded to half) on
+    random scores, on every threshold and on its f32 neighbours."""
+    import numpy as np
+    from factors_of_serendipity_recommendation_amd import _lib
+    L = _lib.lib()
+    min16 = np.float16(mn)
+    inter16 = (np.float16(mx) + np.float16(0.1) - min16) / np.float16(num_fold)
+    thr = (ctypes.c_float * num_fold)()
+    assert L.lgx_strat_thresholds(float(min16), float(inter16), num_fold, thr) == 0
+    t = np.array(thr[:], dtype=np.float32)
+    assert (np.diff(t) >= 0).all()
+    rng = np.random.default_rng(num_fold)
+    fin = t[np.isfinite(t)]
+    s = np.concatenate([rng.uniform(mn - 1.0, mx + 1.0, 200_000).astype(np.float32), fin,
+                        np.nextafter(fin, -np.inf, dtype=np.float32), np.nextafter(fin, np.inf, dtype=np.float32),
+                        np.array([mn, mx, -1e30, 1e30], dtype=np.float32)])
+    with np.errstate(over="ignore", invalid="ignore"):
+        q = np.floor((s.astype(np.float16) - min16) / inter16).astype(np.float64)
+    ref = np.clip(np.nan_to_num(q, nan=num_fold, posinf=num_fold, neginf=0), 0, num_fold).astype(np.int64)
+    got = (s[:, None] >= t[None, :]).sum(1)
+    assert np.array_equal(got, ref)

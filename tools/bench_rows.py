@@ -365,21 +365,33 @@ def row_f4(rows, reps):
         _lib.check(L.lgx_strat_labels(S.data_ptr(), B, I, min16, inter16, F, mp.data_ptr(), mi.data_ptr(),
                                       labels.data_ptr(), hist.data_ptr(), st), "lgx_strat_labels")
 
+    def fused():
+        _lib.check(L.lgx_strat_labels_fused(eu.data_ptr(), None, ei.data_ptr(), B, I, d, _lib.LGX_DTYPE_F32, min16,
+                                            inter16, F, mp.data_ptr(), mi.data_ptr(), labels.data_ptr(),
+                                            hist.data_ptr(), st), "lgx_strat_labels_fused")
+
+    def hist_only():
+        _lib.check(L.lgx_strat_hist(labels.data_ptr(), B, I, F, None, None, hist.data_ptr(), st), "lgx_strat_hist")
+
     def sel():
         _lib.check(L.lgx_strat_select(labels.data_ptr(), B, I, hist.data_ptr(), F + 1, tgt.data_ptr(), 77,
                                       out.data_ptr(), Kc, cnt.data_ptr(), st), "lgx_strat_select")
     ms_s = gpu_ms(lambda: ops.score_dense(eu, ei), reps)
     ms_l = gpu_ms(lab, reps)
+    ms_f = gpu_ms(fused, reps)
+    ms_h = gpu_ms(hist_only, reps)
+    fused()
     ms_p = gpu_ms(sel, reps)
     n = 200
     eu_h, ei_h = eu[:n].cpu().numpy(), ei.cpu().numpy()
     tr = mi[:n * 50].cpu().numpy().reshape(n, 50).tolist()
     s = cpu_s(lambda: oracle.stratification_labels(eu_h, ei_h, tr, F, 0.1))
-    emit(rows, "f4 stratified candidates: scores + labels + select (lgx_score_dense, lgx_strat_labels, "
-         "lgx_strat_select)", ms_s + ms_l + ms_p, B * I, "user-item pairs/s", "hbm", B * I * (4 + 4 + 1 + 1),
+    emit(rows, "f4 stratified candidates: fused scores->labels + select (lgx_strat_labels_fused, "
+         "lgx_strat_select)", ms_f + ms_p, B * I, "user-item pairs/s", "mfma_f32", 2.0 * B * I * d,
          n * I, s, f"{n} users x {I} items: numpy dot + float16 labels + histograms (labels only)", 1,
-         f"per batch: score_dense {ms_s:.2f} ms, labels {ms_l:.2f} ms, select {ms_p:.2f} ms; algorithmic "
-         "10 B per pair (score write + read, label write + read)")
+         f"per batch: fused labels {ms_f:.2f} ms (of which the histogram pass {ms_h:.2f} ms), select "
+         f"{ms_p:.2f} ms; the two-step path: score_dense {ms_s:.2f} + labels {ms_l:.2f} ms; roofline: the "
+         "fused kernel's f32 MFMA flops over the whole batch time")
     del S, labels
     torch.cuda.empty_cache()
 
