@@ -106,11 +106,12 @@ def measured_traffic(config: str, dtype: str, world: int, kernels) -> tuple:
     return b / 1e9, src
 
 
-def epilogue_bytes(mode: int, rows: int, d: int, s: int) -> int:
+def epilogue_bytes(mode: int, rows: int, d: int, s: int, n_prev: int = 0) -> int:
     """Bytes the layer epilogue moves per mode (ops.propagate_layer modes, spmm.hip finish_chunk)."""
     t, f = rows * d * s, rows * d * 4
     return {_lib.LGX_LAYER_PLAIN: t, _lib.LGX_LAYER_FIRST: t + t + f, _lib.LGX_LAYER_MID: t + 2 * f,
-            _lib.LGX_LAYER_LAST: 2 * f, _lib.LGX_LAYER_ONLY: t + f, _lib.LGX_LAYER_PARTIAL: f}[mode]
+            _lib.LGX_LAYER_LAST: 2 * f, _lib.LGX_LAYER_ONLY: t + f, _lib.LGX_LAYER_PARTIAL: f,
+            _lib.LGX_LAYER_STACK: t * (1 + n_prev) + f}[mode]
 
 
 def cold_gather_rows(A, d: int, s: int) -> tuple:
@@ -126,10 +127,10 @@ def cold_gather_rows(A, d: int, s: int) -> tuple:
     return total - hot, R, hot / max(1, total)
 
 
-def layer_models(A, d: int, s: int, mode: int) -> dict:
+def layer_models(A, d: int, s: int, mode: int, n_prev: int = 0) -> dict:
     nnz, rows, N = A.nnz, A.n_rows, A.n_cols
     csr = nnz * 8 + 8 * (rows + 1)
-    epi = epilogue_bytes(mode, rows, d, s)
+    epi = epilogue_bytes(mode, rows, d, s, n_prev)
     cold, R, hot_frac = cold_gather_rows(A, d, s)
     return {"model": csr + epi + cold * d * s, "gathered": csr + epi + nnz * d * s,
             "floor": nnz * 8 + 2 * N * d * s, "hot_rows": R, "hot_frac": hot_frac}
@@ -150,27 +151,31 @@ def make_step(A, E0, K, d, dtype, world, cfg, rank, timings):
     es = 2 if dtype == torch.bfloat16 else 4
     N = A.n_rows if world == 1 else None
     if world == 1:
+        # lgx_propagate's schedule: layers 1..K-1 keep their tables (PLAIN), the last layer forms the
+        # mean from E0 and them (STACK) -- no f32 running sum moved by every layer
         out = torch.empty((N, d), dtype=torch.float32, device="cuda")
-        bufs = [torch.empty((N, d), dtype=dtype, device="cuda") for _ in range(2)]
-        acc = torch.empty((N, d), dtype=torch.float32, device="cuda")
+        bufs = [torch.empty((N, d), dtype=dtype, device="cuda") for _ in range(max(1, K - 1))]
         models = {}
 
         def step(record):
             X = E0
             for k in range(1, K + 1):
-                mode = (_lib.LGX_LAYER_ONLY if K == 1 else _lib.LGX_LAYER_FIRST if k == 1
-                        else _lib.LGX_LAYER_LAST if k == K else _lib.LGX_LAYER_MID)
-                Y = bufs[k & 1] if k < K else None
+                mode = (_lib.LGX_LAYER_ONLY if K == 1 else _lib.LGX_LAYER_STACK if k == K else _lib.LGX_LAYER_PLAIN)
                 if record:
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
-                ops.propagate_layer(A, X, mode, Y=Y, E0=E0, acc=acc, out=out, n_mean=float(K + 1))
+                if mode == _lib.LGX_LAYER_STACK:
+                    ops.propagate_layer_stack(A, X, E0, bufs[:K - 1], out, float(K + 1))
+                else:
+                    ops.propagate_layer(A, X, mode, Y=bufs[k - 1] if k < K else None, E0=E0, out=out,
+                                        n_mean=float(K + 1))
                 if record:
                     e1.record()
                     if mode not in models:
-                        models[mode] = layer_models(A, d, es, mode)
+                        models[mode] = layer_models(A, d, es, mode, K - 1)
                     timings.append((e0, e1, models[mode]))
-                X = Y
+                if k < K:
+                    X = bufs[k - 1]
         return step, A.nnz, A.n_rows
     shard = make_shard(A, cfg.n_users, cfg.n_items, rank, world)
     prop = ShardedPropagation(shard, E0[:cfg.n_users], E0[cfg.n_users:], K)

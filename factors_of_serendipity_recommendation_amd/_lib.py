@@ -20,7 +20,7 @@ CSRC = os.path.join(_HERE, "csrc")
 LGX_OK = 0
 LGX_DTYPE_F32 = 0
 LGX_DTYPE_BF16 = 1
-LGX_LAYER_PLAIN, LGX_LAYER_FIRST, LGX_LAYER_MID, LGX_LAYER_LAST, LGX_LAYER_ONLY, LGX_LAYER_PARTIAL = range(6)
+LGX_LAYER_PLAIN, LGX_LAYER_FIRST, LGX_LAYER_MID, LGX_LAYER_LAST, LGX_LAYER_ONLY, LGX_LAYER_PARTIAL, LGX_LAYER_STACK = range(7)
 LGX_REDUCE_MAX, LGX_REDUCE_SUM = 0, 1
 LGX_STRAT_EXACT = 1
 
@@ -55,6 +55,8 @@ SIGNATURES = {
     "lgx_propagate_layer": (_c_int, [ctypes.POINTER(LgxCSR), _vp, _vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int,
                                      ctypes.c_float, _vp]),
     "lgx_spmm_csr": (_c_int, [ctypes.POINTER(LgxCSR), _vp, _vp, _c_i64, _c_int, _vp]),
+    "lgx_propagate_layer_stack": (_c_int, [ctypes.POINTER(LgxCSR), _vp, _vp, _vp, _c_int, _vp, _c_i64, _c_int,
+                                           ctypes.c_float, _vp]),
     "lgx_strat_labels": (_c_int, [_vp, _c_i64, _c_i64, _c_float, _c_float, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "lgx_strat_select": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_int, _vp, ctypes.c_uint64, _vp, _c_int, _vp, _vp]),
     "lgx_spmm_kernel_name": (_c_int, [_c_i64, _c_int, _c_i64, ctypes.c_char_p, ctypes.c_size_t]),

@@ -857,7 +857,12 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
     // this wave's pieces of a tile: LDS slot q = piece*64 + lane holds 16-B chunk (q % CPR) of tile
     // row q / CPR, fetched from source chunk (q % CPR) ^ (row & SWZ) (the swizzle lives on the source
     // side because the DMA's LDS destination is lane-linear)
-    const int my_pieces = max(0, min(G::PPW, G::PIECES - wave * G::PPW));
+    // DMAPOS 2 / 3 (development): only the upper / lower half of the waves issues the tile DMA
+    constexpr int DW = DMAPOS == 2 || DMAPOS == 3 ? WAVES / 2 : WAVES;  // 4: all waves, this path
+    constexpr int PPW = (G::PIECES + DW - 1) / DW;
+    const bool issuer = DMAPOS == 2 ? wave >= WAVES / 2 : (DMAPOS == 3 ? wave < WAVES / 2 : true);
+    const int dw = DMAPOS == 2 ? wave - WAVES / 2 : wave;
+    const int my_pieces = issuer ? max(0, min(PPW, G::PIECES - dw * PPW)) : 0;
     const uint32_t lds_tiles = lds_u32(tiles);
 
     auto tile_start = [&](int64_t t) {
@@ -875,17 +880,17 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
             const bool tail = t0 + G::TILE_ITEMS > i_end;
             const int last = (int)(i_end - 1 - t0);  // tail rows re-read the split's last row (masked later)
             // offsets recomputed per tile: cheaper than holding them in registers
-            const int q = (wave * G::PPW + p) * 64 + lane;
+            const int q = (dw * PPW + p) * 64 + lane;
             const int row = q / G::CPR;
             const int src = (q % G::CPR) ^ (row & G::SWZ);
             const int srow = tail && row > last ? last : row;
             lds_dma16(base, (uint32_t)(srow * G::RB + src * 16),
-                      __builtin_amdgcn_readfirstlane(lds_tiles + buf * G::TILE + (wave * G::PPW + p) * 1024));
+                      __builtin_amdgcn_readfirstlane(lds_tiles + buf * G::TILE + (dw * PPW + p) * 1024));
         }
     };
     auto stage = [&](int buf, int64_t t0) {
 #pragma unroll
-        for (int p = 0; p < G::PPW; ++p) stage_piece(buf, t0, p);
+        for (int p = 0; p < PPW; ++p) stage_piece(buf, t0, p);
     };
 
     const int ahead = nbuf - 1;
@@ -1032,7 +1037,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
         const int64_t t0 = tile_start(t);
         refill = ABLATE != 5 && ABLATE != 7 && t + ahead < ntiles;
         if (refill) refill_t0 = tile_start(ABLATE == 6 ? 0 : t + ahead);  // 6 (development): L2-hot refills
-        if (DMAPOS == 0 && refill) stage(sbuf, refill_t0);
+        if (DMAPOS != 1 && refill) stage(sbuf, refill_t0);
 #ifdef LGX_SCORE_STATS
         const uint64_t ep_t0_ = __builtin_amdgcn_s_memtime();
 #endif

@@ -117,7 +117,10 @@ struct LayerArgs {
     int64_t d;
     int mode;
     float n_mean;
+    const void* prev[7];  // LGX_LAYER_STACK: the kept layer tables
+    int n_prev;
 };
+constexpr int kMaxPrev = 7;
 
 // finish one 16-B chunk (VEC values, columns [off, off+VEC)) of output row `row`
 template <typename T>
@@ -160,6 +163,24 @@ __device__ __forceinline__ void finish_chunk(const LayerArgs& a, int64_t row, in
                 s.w = (s.w + v[j + 3]) / a.n_mean;
                 *reinterpret_cast<float4*>(a.out + o + j) = s;
             }
+            break;
+        }
+        case LGX_LAYER_STACK: {
+            float e[VEC];
+            Vec<T>::load(static_cast<const T*>(a.E0) + o, e);
+#pragma unroll
+            for (int p = 0; p < kMaxPrev; ++p) {  // static indices: the table pointers stay in SGPRs
+                if (p >= a.n_prev) break;
+                float y[VEC];
+                Vec<T>::load(static_cast<const T*>(a.prev[p]) + o, y);
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) e[j] += y[j];
+            }
+#pragma unroll
+            for (int j = 0; j < VEC; j += 4)
+                *reinterpret_cast<float4*>(a.out + o + j) =
+                    make_float4((e[j] + v[j]) / a.n_mean, (e[j + 1] + v[j + 1]) / a.n_mean,
+                                (e[j + 2] + v[j + 2]) / a.n_mean, (e[j + 3] + v[j + 3]) / a.n_mean);
             break;
         }
         case LGX_LAYER_PARTIAL: {
@@ -416,7 +437,27 @@ extern "C" int lgx_propagate_layer(const lgx_csr* A, const void* X, void* Y, con
     if (A->n_rows == 0) return LGX_OK;
     LayerArgs a{A->indptr, A->indices, A->vals, A->seg_row, A->seg_part, A->seg_slot, A->n_segs,
                 A->seg_len, A->split_row, A->split_ptr, A->n_split, A->partials,
-                X, Y, E0, acc, out, d, mode, n_mean};
+                X, Y, E0, acc, out, d, mode, n_mean, {}, 0};
+    if (dtype == LGX_DTYPE_F32) return dispatch_layer<float>(a, as_hip(stream));
+    return dispatch_layer<uint16_t>(a, as_hip(stream));
+}
+
+extern "C" int lgx_propagate_layer_stack(const lgx_csr* A, const void* X, const void* E0, const void* const* prev,
+                                         int n_prev, float* out, int64_t d, int dtype, float n_mean,
+                                         lgx_stream_t stream) {
+    int rc = check_csr(A, d, dtype);
+    if (rc) return rc;
+    LGX_REQUIRE(n_prev >= 0 && n_prev <= kMaxPrev && (n_prev == 0 || prev), LGX_ERR_INVALID_ARG,
+                "lgx_propagate_layer_stack: n_prev %d outside [0, %d]", n_prev, kMaxPrev);
+    LGX_REQUIRE((X || A->nnz == 0) && E0 && out && n_mean > 0.0f, LGX_ERR_INVALID_ARG,
+                "lgx_propagate_layer_stack: bad arguments");
+    for (int p = 0; p < n_prev; ++p)
+        LGX_REQUIRE(prev[p], LGX_ERR_INVALID_ARG, "lgx_propagate_layer_stack: prev[%d] is null", p);
+    if (A->n_rows == 0) return LGX_OK;
+    LayerArgs a{A->indptr, A->indices, A->vals, A->seg_row, A->seg_part, A->seg_slot, A->n_segs,
+                A->seg_len, A->split_row, A->split_ptr, A->n_split, A->partials,
+                X, nullptr, E0, nullptr, out, d, LGX_LAYER_STACK, n_mean, {}, n_prev};
+    for (int p = 0; p < n_prev; ++p) a.prev[p] = prev[p];
     if (dtype == LGX_DTYPE_F32) return dispatch_layer<float>(a, as_hip(stream));
     return dispatch_layer<uint16_t>(a, as_hip(stream));
 }
@@ -516,9 +557,24 @@ extern "C" int lgx_propagate(const lgx_csr* A, const void* E0, float* out, int64
     LGX_REQUIRE(ws && ws_bytes >= need, LGX_ERR_WORKSPACE, "lgx_propagate: workspace %zu < %zu", ws_bytes, need);
     const size_t es = dtype == LGX_DTYPE_F32 ? 4 : 2;
     char* base = static_cast<char*>(ws);
-    void* buf[2] = {base, base + align_up(N * d * es)};
-    float* acc = reinterpret_cast<float*>(base + 2 * align_up(N * d * es));
     const float n_mean = (float)(K + 1);
+    // keep the K-1 intermediate tables when they fit the workspace: the last layer forms the mean
+    // from them (no f32 running sum read and written by every layer)
+    const size_t tbl = align_up(N * d * es);
+    if (K >= 2 && K - 1 <= kMaxPrev && (size_t)(K - 1) * tbl <= ws_bytes) {
+        const void* prev[kMaxPrev];
+        const void* X = E0;
+        for (int k = 1; k < K; ++k) {
+            void* Y = base + (size_t)(k - 1) * tbl;
+            rc = lgx_propagate_layer(A, X, Y, nullptr, nullptr, nullptr, d, dtype, LGX_LAYER_PLAIN, 1.0f, stream_);
+            if (rc) return rc;
+            prev[k - 1] = Y;
+            X = Y;
+        }
+        return lgx_propagate_layer_stack(A, X, E0, prev, K - 1, out, d, dtype, n_mean, stream_);
+    }
+    void* buf[2] = {base, base + tbl};
+    float* acc = reinterpret_cast<float*>(base + 2 * tbl);
     const void* X = E0;
     for (int k = 1; k <= K; ++k) {
         int mode;

@@ -42,6 +42,19 @@ def propagate_layer(A: CSRGraph, X: torch.Tensor, mode: int, Y: Optional[torch.T
                "lgx_propagate_layer")
 
 
+def propagate_layer_stack(A: CSRGraph, X: torch.Tensor, E0: torch.Tensor, prev: Sequence[torch.Tensor],
+                          out: torch.Tensor, n_mean: float) -> None:
+    """The last layer over kept layer tables (``lgx_propagate_layer_stack``):
+    out = (E0 + prev[0] + ... + prev[-1] + A X) / n_mean."""
+    require_gpu(X, E0, out, *prev)
+    d = X.shape[1]
+    cs = A.c_struct(d)
+    arr = (ctypes.c_void_p * max(1, len(prev)))(*[p.data_ptr() for p in prev])
+    _lib.check(_lib.lib().lgx_propagate_layer_stack(ctypes.byref(cs), _ptr(X), _ptr(E0), arr, len(prev), _ptr(out),
+                                                    d, _dtype_code(X), float(n_mean), _stream_ptr(X.device)),
+               "lgx_propagate_layer_stack")
+
+
 def layer_epilogue(y: torch.Tensor, mode: int, Y: Optional[torch.Tensor] = None, E0: Optional[torch.Tensor] = None,
                    acc: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, n_mean: float = 1.0,
                    dtype: Optional[torch.dtype] = None) -> None:

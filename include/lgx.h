@@ -62,6 +62,8 @@ typedef struct ihipStream_t* lgx_stream_t; /* == hipStream_t */
 #define LGX_LAYER_ONLY 4  /* out = (E0 + A X) / n_mean           (K == 1, Y not written) */
 #define LGX_LAYER_PARTIAL 5 /* out = A X in fp32, nothing else (a rank's partial sums of a
                                row-sharded push, reduced across ranks before the epilogue)   */
+#define LGX_LAYER_STACK 6 /* out = (E0 + prev[0] + .. + prev[n-1] + A X) / n_mean, the last layer
+                             over the kept layer tables (lgx_propagate_layer_stack only)      */
 
 /*
  * A row-partitioned CSR operator plus its launch plan.
@@ -146,11 +148,22 @@ int lgx_layer_epilogue(const float* y, int64_t rows, void* Y, const void* E0, fl
  * kernel a benchmark configuration times.  No device work.
  */
 int lgx_spmm_kernel_name(int64_t d, int dtype, int64_t seg_len, char* buf, size_t len);
+/*
+ * The last layer over kept layer tables: out = (E0 + prev[0] + ... + prev[n_prev-1] + A X) / n_mean,
+ * summed in that order in fp32 (for fp32 storage the same bits as the FIRST / MID / LAST chain).
+ * prev: host array of n_prev <= 7 device pointers to [n_rows, d] dtype tables (PLAIN outputs).
+ * Per layer this moves (n_prev + 1) dtype tables + one f32 table instead of an f32 running sum
+ * read and written every layer.
+ */
+int lgx_propagate_layer_stack(const lgx_csr* A, const void* X, const void* E0, const void* const* prev,
+                              int n_prev, float* out, int64_t d, int dtype, float n_mean, lgx_stream_t stream);
 /* Y = A X (alias of lgx_propagate_layer with LGX_LAYER_PLAIN). */
 int lgx_spmm_csr(const lgx_csr* A, const void* X, void* Y, int64_t d, int dtype, lgx_stream_t stream);
 /* Workspace bytes of lgx_propagate: 2 x [N,d] dtype ping-pong tables + [N,d] f32 layer sum. */
 int lgx_propagate_workspace(int64_t n_rows, int64_t d, int dtype, size_t* ws_bytes);
-/* Whole K-layer propagation (square A, X = E0 table [N,d] dtype) -> out [N,d] f32 layer mean. */
+/* Whole K-layer propagation (square A, X = E0 table [N,d] dtype) -> out [N,d] f32 layer mean.
+ * When the K-1 intermediate tables fit the workspace (bf16: K <= 5, f32: K <= 4) they are kept
+ * and the last layer forms the mean (LGX_LAYER_STACK); otherwise the f32 running sum. */
 int lgx_propagate(const lgx_csr* A, const void* E0, float* out, int64_t d, int K, int dtype,
                   void* ws, size_t ws_bytes, lgx_stream_t stream);
 

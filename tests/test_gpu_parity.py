@@ -200,6 +200,40 @@ def test_layer_modes_compose(mlls):
     assert torch.equal(out, lgx.propagate(A, E0, 1))
 
 
+@pytest.mark.parametrize("K", [2, 3, 4, 5, 7])
+def test_kept_tables_schedule_equals_running_sum(mlls, K):
+    """lgx_propagate keeps the K-1 layer tables and forms the mean in the last layer
+    (LGX_LAYER_STACK) when they fit its workspace (f32: K <= 4); with fp32 storage that is the
+    FIRST / MID / LAST running-sum chain bit for bit.  K = 5, 7 take the running sum itself."""
+    U, I = int(mlls["n_users"]), int(mlls["n_items"])
+    A = lgx.build_norm_adj(mlls["train_users"], mlls["train_items"], U, I, dedup=True, device=DEV)
+    E0 = torch.from_numpy(np.concatenate([mlls["emb_user"], mlls["emb_item"]])).to(DEV)
+    acc, out = torch.empty_like(E0), torch.empty_like(E0)
+    X = E0
+    for k in range(1, K + 1):
+        mode = _lib.LGX_LAYER_FIRST if k == 1 else _lib.LGX_LAYER_LAST if k == K else _lib.LGX_LAYER_MID
+        Y = torch.empty_like(E0) if k < K else None
+        ops.propagate_layer(A, X, mode, Y=Y, E0=E0, acc=acc, out=out, n_mean=float(K + 1))
+        X = Y
+    assert torch.equal(lgx.propagate(A, E0, K), out)
+    # the stacked last layer by hand, bf16 tables: the mean of the stored layers
+    Eb = E0.to(torch.bfloat16)
+    tabs, X = [], Eb
+    for k in range(1, K):
+        Y = torch.empty_like(Eb)
+        ops.propagate_layer(A, X, _lib.LGX_LAYER_PLAIN, Y=Y)
+        tabs.append(Y)
+        X = Y
+    outb = torch.empty_like(E0)
+    ops.propagate_layer_stack(A, X, Eb, tabs, outb, float(K + 1))
+    last = torch.empty_like(Eb)
+    ops.propagate_layer(A, X, _lib.LGX_LAYER_PLAIN, Y=last)  # bf16-rounded copy of the last layer
+    ref = (Eb.float() + sum(t.float() for t in tabs) + last.float()) / (K + 1)
+    assert torch.allclose(outb, ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+    if K <= 5:
+        assert torch.equal(lgx.propagate(A, Eb, K), outb)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_partial_plus_epilogue_equals_fused_layer(mlls, dt):
     """PARTIAL (fp32 A X) followed by lgx_layer_epilogue == the fused layer, bit for bit, in every
