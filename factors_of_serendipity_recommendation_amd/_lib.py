@@ -67,6 +67,7 @@ SIGNATURES = {
                                         _vp, _vp, _vp, _vp, _vp]),
     "lgx_strat_thresholds": (_c_int, [_c_float, _c_float, _c_int, _vp]),
     "lgx_strat_hist": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _vp, _vp, _vp, _vp]),
+    "lgx_strat_mask": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _vp, _vp, _vp, _vp]),
     "lgx_parse_lines_workspace": (_c_int, [_c_i64, _sz_p]),
     "lgx_parse_lines_count": (_c_int, [_vp, _c_i64, _vp, ctypes.c_size_t, _vp, _vp]),
     "lgx_parse_lines_fill": (_c_int, [_vp, _c_i64, _vp, ctypes.c_size_t, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp]),
@@ -78,6 +79,8 @@ SIGNATURES = {
                                        _vp, _vp, _vp, _vp]),
     "lgx_adam_step": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                ctypes.c_double, _c_i64, _vp]),
+    "lgx_adam_step_dev": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                   ctypes.c_double, _vp, _vp]),
     "lgx_list_dot_reduce": (_c_int, [_vp, _c_i64, _c_int, _c_i64, _vp, _vp, _vp, _vp, _c_int, _vp, _vp]),
     "lgx_layer_epilogue": (_c_int, [_vp, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_float, _vp]),
     "lgx_propagate_workspace": (_c_int, [_c_i64, _c_i64, _c_int, _sz_p]),

@@ -288,8 +288,56 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     }
 }
 
+// the same step with t read from device memory (a graph-captured training step replays with the
+// counter the captured add advanced): the bias corrections in double per thread, rounded once
+struct AdamDevArgs {
+    float w1, beta2, w2, eps;
+    double lr, b1, b2;
+};
+__global__ __launch_bounds__(256) void adam_kernel_dev(float* __restrict__ p, const float* __restrict__ g,
+                                                      float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                      AdamDevArgs h, const float* __restrict__ step) {
+    const double t = (double)*step;
+    const AdamArgs a{h.w1, h.beta2, h.w2, (float)(h.lr / (1.0 - pow(h.b1, t))), (float)sqrt(1.0 - pow(h.b2, t)),
+                     h.eps};
+    const int64_t i4 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t i = i4 * 4;
+    if (i + 3 < n) {
+        float4 P = reinterpret_cast<float4*>(p)[i4];
+        const float4 G = reinterpret_cast<const float4*>(g)[i4];
+        float4 M = reinterpret_cast<float4*>(m)[i4];
+        float4 V = reinterpret_cast<float4*>(v)[i4];
+        adam_one(P.x, G.x, M.x, V.x, a);
+        adam_one(P.y, G.y, M.y, V.y, a);
+        adam_one(P.z, G.z, M.z, V.z, a);
+        adam_one(P.w, G.w, M.w, V.w, a);
+        reinterpret_cast<float4*>(p)[i4] = P;
+        reinterpret_cast<float4*>(m)[i4] = M;
+        reinterpret_cast<float4*>(v)[i4] = V;
+    } else {
+        for (int64_t j = i; j < n; ++j) adam_one(p[j], g[j], m[j], v[j], a);
+    }
+}
+
 }  // namespace
 }  // namespace lgx
+
+extern "C" int lgx_adam_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                                 double lr, double beta1, double beta2, double eps, const float* step,
+                                 lgx_stream_t stream) {
+    LGX_REQUIRE(n >= 0 && lr >= 0.0 && beta1 >= 0.0 && beta1 < 1.0 && beta2 >= 0.0 && beta2 < 1.0, LGX_ERR_INVALID_ARG,
+                "lgx_adam_step_dev: bad arguments");
+    if (n == 0) return LGX_OK;
+    LGX_REQUIRE(param && grad && exp_avg && exp_avg_sq && step, LGX_ERR_INVALID_ARG, "lgx_adam_step_dev: null pointer");
+    LGX_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0,
+                LGX_ERR_INVALID_ARG, "lgx_adam_step_dev: tensors must be 16-byte aligned");
+    AdamDevArgs h{(float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps, lr, beta1, beta2};
+    const int64_t n4 = ceil_div(n, (int64_t)4);
+    adam_kernel_dev<<<(unsigned)ceil_div(n4, (int64_t)256), 256, 0, as_hip(stream)>>>(param, grad, exp_avg, exp_avg_sq,
+                                                                                      n, h, step);
+    LGX_LAUNCH_CHECK();
+    return LGX_OK;
+}
 
 extern "C" int lgx_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, double lr,
                              double beta1, double beta2, double eps, int64_t step, lgx_stream_t stream) {

@@ -1361,11 +1361,16 @@ inline bool strat_estimate_within_one(const StratThr& thr) {
     }
 }
 
+// label counts of the workgroup's 256 users kept in LDS (stride 17: the 32 users of a wave sit in
+// 32 different banks), added to the global histogram once per workgroup
+constexpr int kHistStride = 17;
+
 template <int DT, int KCH, bool VEC4, bool EST1>
 __global__ __launch_bounds__(kDenseWaves * 64) void strat_label_lds(const void* Q, const int64_t* user_rows,
                                                                      const void* items, int64_t B, int64_t n_items,
                                                                      int64_t d, StratThr thr,
-                                                                     int8_t* __restrict__ labels, int64_t n_ug,
+                                                                     int8_t* __restrict__ labels,
+                                                                     int32_t* __restrict__ hist, int64_t n_ug,
                                                                      int64_t split_items) {
     static_assert(KCH >= 8, "swizzle needs >= 16 slots per row");
     typedef Frag<DT> F;
@@ -1378,10 +1383,13 @@ __global__ __launch_bounds__(kDenseWaves * 64) void strat_label_lds(const void* 
     // T[j] = the score where label j starts (T[0] = -inf, T[n + 1] = +inf): the label of s is the
     // estimate e corrected by one compare on each side, s < T[e] and s >= T[e + 1]
     __shared__ float T[34];
+    __shared__ uint32_t hc[kDenseUsers * kHistStride];  // hist != nullptr: per-user label counts
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, col = lane & 31;
     if (threadIdx.x < 34)
         T[threadIdx.x] = threadIdx.x == 0 ? -INFINITY : (threadIdx.x <= thr.n ? thr.t[threadIdx.x - 1] : INFINITY);
+    if (hist)
+        for (int e = threadIdx.x; e < kDenseUsers * kHistStride; e += kDenseWaves * 64) hc[e] = 0u;
     const int64_t L = blockIdx.x, kk = L >> 3;
     const int64_t ug = kk % n_ug;
     const int64_t split = (kk / n_ug) * 8 + (L & 7);
@@ -1448,11 +1456,19 @@ __global__ __launch_bounds__(kDenseWaves * 64) void strat_label_lds(const void* 
                 acc = F::mma(__builtin_bit_cast(typename F::chunk, fr), uf[c], acc);
             }
             if (user_ok) {
+                uint32_t* hu = hc + (wave * kUsersPerWave + col) * kHistStride;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int64_t it = i0 + 8 * q + 4 * h;  // items it .. it + 3: acc rows 4q .. 4q + 3
-                    const uint32_t w = label(acc[4 * q]) | (label(acc[4 * q + 1]) << 8) |
-                                       (label(acc[4 * q + 2]) << 16) | (label(acc[4 * q + 3]) << 24);
+                    const uint32_t l0 = label(acc[4 * q]), l1 = label(acc[4 * q + 1]);
+                    const uint32_t l2 = label(acc[4 * q + 2]), l3 = label(acc[4 * q + 3]);
+                    const uint32_t w = l0 | (l1 << 8) | (l2 << 16) | (l3 << 24);
+                    if (hist) {  // items past the split's end are not counted
+                        if (it < i_end) atomicAdd(hu + l0, 1u);
+                        if (it + 1 < i_end) atomicAdd(hu + l1, 1u);
+                        if (it + 2 < i_end) atomicAdd(hu + l2, 1u);
+                        if (it + 3 < i_end) atomicAdd(hu + l3, 1u);
+                    }
                     if (VEC4 && it + 4 <= i_end) {
                         *reinterpret_cast<uint32_t*>(lab + it) = w;
                     } else {
@@ -1466,6 +1482,14 @@ __global__ __launch_bounds__(kDenseWaves * 64) void strat_label_lds(const void* 
         if (more) store_tile(buf ^ 1);
         __syncthreads();
         buf ^= 1;
+    }
+    if (hist) {  // the loop's last barrier has published every count
+        const int64_t ub = ug * kDenseUsers;
+        for (int e = threadIdx.x; e < kDenseUsers * kHistStride; e += kDenseWaves * 64) {
+            const int uu = e / kHistStride, l = e % kHistStride;
+            const uint32_t c = hc[e];
+            if (c && l <= thr.n && ub + uu < B) atomicAdd(hist + (ub + uu) * (thr.n + 1) + l, (int32_t)c);
+        }
     }
 }
 
@@ -1860,13 +1884,16 @@ extern "C" int lgx_strat_labels_fused(const void* Q, const int64_t* user_rows, c
     LGX_REQUIRE(grid < (1LL << 31), LGX_ERR_UNSUPPORTED, "lgx_strat_labels_fused: %lld users is too many", (long long)B);
     const bool vec4 = n_items % 4 == 0 && ((uintptr_t)labels & 3) == 0;
     const bool est1 = strat_estimate_within_one(thr);
+    // counts in the scoring kernel (num_fold + 1 <= 17 bins), else a counting pass over the labels
+    const bool fuse_hist = num_fold + 1 <= kHistStride;
+    if (fuse_hist) LGX_HIP_CHECK(hipMemsetAsync(hist, 0, (size_t)B * (num_fold + 1) * sizeof(int32_t), stream));
 #define LGX_SL3(DTV, KC, V4)                                                                                      \
     if (est1)                                                                                                     \
         strat_label_lds<DTV, KC, V4, true><<<(unsigned)grid, kDenseWaves * 64, 0, stream>>>(                      \
-            Q, user_rows, items, B, n_items, d, thr, labels, n_ug, split_items);                                  \
+            Q, user_rows, items, B, n_items, d, thr, labels, fuse_hist ? hist : nullptr, n_ug, split_items);      \
     else                                                                                                          \
         strat_label_lds<DTV, KC, V4, false><<<(unsigned)grid, kDenseWaves * 64, 0, stream>>>(                     \
-            Q, user_rows, items, B, n_items, d, thr, labels, n_ug, split_items)
+            Q, user_rows, items, B, n_items, d, thr, labels, fuse_hist ? hist : nullptr, n_ug, split_items)
 #define LGX_SL2(DTV, KC, V4) do { LGX_SL3(DTV, KC, V4); } while (0)
 #define LGX_SL_ALL(DTV)                                                              \
     switch (kch) {                                                                   \
@@ -1879,5 +1906,6 @@ extern "C" int lgx_strat_labels_fused(const void* Q, const int64_t* user_rows, c
 #undef LGX_SL2
 #undef LGX_SL3
     LGX_LAUNCH_CHECK();
+    if (fuse_hist) return lgx_strat_mask(labels, B, n_items, num_fold, mask_indptr, mask_indices, hist, stream_);
     return lgx_strat_hist(labels, B, n_items, num_fold, mask_indptr, mask_indices, hist, stream_);
 }

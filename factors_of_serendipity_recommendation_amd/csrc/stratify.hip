@@ -22,6 +22,7 @@
 
 #include <hip/hip_fp16.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <cstring>
 
@@ -162,6 +163,27 @@ __global__ __launch_bounds__(kStratThreads) void strat_hist_kernel(int8_t* __res
     }
     __syncthreads();
     if (threadIdx.x <= num_fold) hist[u * (num_fold + 1) + threadIdx.x] = h[threadIdx.x];
+}
+
+// The masked items of labelled rows relabelled -1 and taken out of the counts: one thread per mask
+// entry (sorted rows: repeats skipped)
+__global__ __launch_bounds__(kStratThreads) void strat_mask_kernel(int8_t* __restrict__ labels, int64_t n_items,
+                                                                  int num_fold,
+                                                                  const int64_t* __restrict__ mask_indptr,
+                                                                  const int32_t* __restrict__ mask_indices,
+                                                                  int32_t* __restrict__ hist) {
+    const int64_t u = blockIdx.y;
+    const int64_t m0 = mask_indptr[u], m1 = mask_indptr[u + 1];
+    for (int64_t j = m0 + (int64_t)blockIdx.x * kStratThreads + threadIdx.x; j < m1;
+         j += (int64_t)gridDim.x * kStratThreads) {
+        const int32_t it = mask_indices[j];
+        if (it < 0 || it >= n_items || (j > m0 && mask_indices[j - 1] == it)) continue;
+        int8_t* p = labels + u * n_items + it;
+        const int l = *p;
+        if (l < 0 || l > num_fold) continue;
+        atomicSub(hist + u * (num_fold + 1) + l, 1);
+        *p = -1;
+    }
 }
 
 // per-user random order of the items: high word = a 32-bit bijection of the item index (odd
@@ -445,6 +467,23 @@ extern "C" int lgx_strat_hist(int8_t* labels, int64_t n_users, int64_t n_items, 
         strat_hist_kernel<false><<<(unsigned)n_users, kStratThreads, 0, as_hip(stream)>>>(
             labels, n_items, num_fold, mask_indptr, mask_indices, hist);
     LGX_LAUNCH_CHECK();
+    return LGX_OK;
+}
+
+extern "C" int lgx_strat_mask(int8_t* labels, int64_t n_users, int64_t n_items, int num_fold,
+                              const int64_t* mask_indptr, const int32_t* mask_indices, int32_t* hist,
+                              lgx_stream_t stream) {
+    LGX_REQUIRE(n_users >= 0 && n_items >= 0 && num_fold >= 1 && num_fold < kMaxFolds, LGX_ERR_INVALID_ARG,
+                "lgx_strat_mask: bad sizes");
+    if (n_users == 0 || !mask_indptr) return LGX_OK;
+    LGX_REQUIRE(labels && hist && mask_indices, LGX_ERR_INVALID_ARG, "lgx_strat_mask: null pointer");
+    // grid.y is capped at 65535: users beyond it go in further launches
+    for (int64_t u0 = 0; u0 < n_users; u0 += 65535) {
+        const int64_t nu = std::min<int64_t>(65535, n_users - u0);
+        strat_mask_kernel<<<dim3(1, (unsigned)nu), kStratThreads, 0, as_hip(stream)>>>(
+            labels + u0 * n_items, n_items, num_fold, mask_indptr + u0, mask_indices, hist + u0 * (num_fold + 1));
+        LGX_LAUNCH_CHECK();
+    }
     return LGX_OK;
 }
 

@@ -261,6 +261,10 @@ int lgx_strat_thresholds(float min16, float inter16, int num_fold, float* thr);
  * out of the counts (the last step of lgx_strat_labels, for labels written by the fused kernel) */
 int lgx_strat_hist(int8_t* labels, int64_t n_users, int64_t n_items, int num_fold, const int64_t* mask_indptr,
                    const int32_t* mask_indices, int32_t* hist, lgx_stream_t stream);
+/* only the mask step of lgx_strat_hist: masked items of labelled rows -> -1, taken out of hist
+ * (for the counts the fused kernel made itself: up to 17 bins) */
+int lgx_strat_mask(int8_t* labels, int64_t n_users, int64_t n_items, int num_fold, const int64_t* mask_indptr,
+                   const int32_t* mask_indices, int32_t* hist, lgx_stream_t stream);
 
 /* ---------------------------------------------------------------- 8(f) rank 3: interaction files */
 /*
@@ -318,6 +322,10 @@ int lgx_bpr_loss_backward(const float* light, const float* ego_user, const float
  */
 int lgx_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, double lr,
                   double beta1, double beta2, double eps, int64_t step, lgx_stream_t stream);
+/* the same with the step count t read from device memory (f32, already advanced for this step), so
+ * that a hipGraph-captured training step replays with a live count */
+int lgx_adam_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, double lr,
+                      double beta1, double beta2, double eps, const float* step, lgx_stream_t stream);
 
 /* ---------------------------------------------------------------- 8(f) rank 1: list x list similarity */
 #define LGX_REDUCE_MAX 0

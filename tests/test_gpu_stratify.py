@@ -144,23 +144,25 @@ def test_fast_select_equals_radix_select():
         assert np.array_equal(fast[0][u, :fast[1][u]], exact[0][u, :exact[1][u]])
 
 
-@pytest.mark.parametrize("dtype,d,I", [(torch.float32, 64, 4096), (torch.float32, 40, 3001), (torch.float32, 128, 3001),
-                                       (torch.float32, 256, 1030), (torch.bfloat16, 128, 4096),
-                                       (torch.bfloat16, 256, 2999)])
-def test_fused_labels_equal_two_step_labels(dtype, d, I):
-    """lgx_strat_labels_fused (scores labelled in the MFMA epilogue) == lgx_score_dense +
-    lgx_strat_labels, label for label and count for count, masked items included; tails where the
-    catalog is not a multiple of 4 / 16."""
+@pytest.mark.parametrize("dtype,d,I,F", [(torch.float32, 64, 4096, 10), (torch.float32, 40, 3001, 10),
+                                         (torch.float32, 128, 3001, 16), (torch.float32, 256, 1030, 10),
+                                         (torch.bfloat16, 128, 4096, 10), (torch.bfloat16, 256, 2999, 10),
+                                         (torch.float32, 64, 3001, 24)])
+def test_fused_labels_equal_two_step_labels(dtype, d, I, F):
+    """lgx_strat_labels_fused (scores labelled and counted in the MFMA epilogue; > 16 folds count
+    in a separate pass) == lgx_score_dense + lgx_strat_labels, label for label and count for count,
+    masked items included; tails where the catalog is not a multiple of 4 / 16; 300 users = one
+    full and one partial 256-user group."""
     eu, ei, train = _setup(seed=d + I, U=300, I=I, d=d)
     Eu, Ei = torch.from_numpy(eu).to(DEV).to(dtype), torch.from_numpy(ei).to(DEV).to(dtype)
-    min16, inter16 = recommend.stratification_bounds(Eu.float(), Ei.float(), 10, 0.1)
+    min16, inter16 = recommend.stratification_bounds(Eu.float(), Ei.float(), F, 0.1)
     mp, mi = ops.lists_to_device_csr(train, DEV)
     assert recommend.fused_labels_eligible(Eu, d)
-    lab_f, hist_f = recommend.strat_labels(Eu, Ei, mp, mi, min16, inter16, 10, fused=True)
-    lab_2, hist_2 = recommend.strat_labels(Eu, Ei, mp, mi, min16, inter16, 10, fused=False)
+    lab_f, hist_f = recommend.strat_labels(Eu, Ei, mp, mi, min16, inter16, F, fused=True)
+    lab_2, hist_2 = recommend.strat_labels(Eu, Ei, mp, mi, min16, inter16, F, fused=False)
     assert torch.equal(lab_f, lab_2)
     assert torch.equal(hist_f, hist_2)
-    assert (lab_f >= -1).all() and (lab_f <= 10).all()
+    assert (lab_f >= -1).all() and (lab_f <= F).all()
 
 
 def test_fused_stratified_candidates_equal_two_step():

@@ -83,6 +83,47 @@ def test_bpr_epoch_through_hip_propagation(mlls, tmp_path):
     assert all(np.isfinite(losses)) and losses[-1] < losses[0], losses
 
 
+def test_captured_epoch_equals_eager_epoch(mlls, tmp_path):
+    """BPR_train_original with the minibatch captured as a hipGraph (the default) against the eager
+    loop, from the same weights and sampler seed: the same parameters after two epochs (to the
+    f32 atomics' summation-order noise of the fused loss backward), the same Adam step count, and
+    the eval-mode propagation cache sees the replayed updates."""
+    from factors_of_serendipity_recommendation_amd.dataloader import Loader
+    from factors_of_serendipity_recommendation_amd.model import LightGCN
+    tp, tx = mlls["train_list_indptr"], mlls["train_list_indices"]
+    with open(tmp_path / "train.txt", "w") as f:
+        for j, u in enumerate(mlls["train_list_users"]):
+            f.write(" ".join(str(x) for x in [u] + list(tx[tp[j]:tp[j + 1]])) + "\n")
+    with open(tmp_path / "test.txt", "w") as f:
+        f.write(f"{int(mlls['train_list_users'][0])} {int(tx[0])}\n")
+    ds = Loader(path=str(tmp_path), device=DEV)
+    cfg = {"latent_dim_rec": 64, "lightGCN_n_layers": 3, "keep_prob": 0.6, "A_split": False, "pretrain": 0,
+           "dropout": 0, "decay": 1e-4, "lr": 0.001}
+    runs = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        model = LightGCN(cfg, ds).to(DEV)
+        bpr = train.BPRLoss(model, cfg)
+        model.eval()
+        with torch.no_grad():
+            before = model.getUsersRating(torch.arange(4, device=DEV)).clone()
+        sampling.seed(7)
+        for epoch in range(2):
+            train.BPR_train_original(ds, model, bpr, epoch, batch_size=512, device=DEV, graph=graph)
+        model.eval()
+        with torch.no_grad():
+            after = model.getUsersRating(torch.arange(4, device=DEV))
+        assert not torch.equal(before, after), "eval cache kept the pre-training propagation"
+        steps = [float(st["step"]) for st in bpr.opt.state.values()]
+        runs.append(([p.detach().clone() for p in model.parameters()], steps))
+    (pe, se), (pg, sg) = runs
+    rows = ds.n_users * max(1, ds.trainDataSize // ds.n_users)  # the epoch's sample rows (train.py)
+    n_batches = 2 * (-(-rows // 512))
+    assert se == sg and all(x == n_batches for x in sg), (se, sg, n_batches)
+    for a, b in zip(pe, pg):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-5 * b.abs().max().item())
+
+
 # ---------------------------------------------------------------- fused BPR loss (csrc/bpr.hip)
 def _torch_bpr(light, wu, wi, users, pos, neg):
     """model.py:196-209 in the reference's torch ops (fp32), the parity reference."""
