@@ -389,7 +389,8 @@ def row_f4(rows, reps):
     emit(rows, "f4 stratified candidates: fused scores->labels + select (lgx_strat_labels_fused, "
          "lgx_strat_select)", ms_f + ms_p, B * I, "user-item pairs/s", "mfma_f32", 2.0 * B * I * d,
          n * I, s, f"{n} users x {I} items: numpy dot + float16 labels + histograms (labels only)", 1,
-         f"per batch: fused labels {ms_f:.2f} ms (of which the histogram pass {ms_h:.2f} ms), select "
+         f"per batch: fused labels + counts {ms_f:.2f} ms (the counting pass over the labels it replaces: "
+         f"{ms_h:.2f} ms), select "
          f"{ms_p:.2f} ms; the two-step path: score_dense {ms_s:.2f} + labels {ms_l:.2f} ms; roofline: the "
          "fused kernel's f32 MFMA flops over the whole batch time")
     del S, labels
