@@ -1028,9 +1028,17 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
             }
             regroup();
         }
+        const float tau_before = st.tau;
         if (tail) st.template block<MINMAX, NACC, false, M16, true>(a, acc0, acc1, e0, i_end);
         else st.template block<MINMAX, NACC, false, M16, false>(a, acc0, acc1, e0, i_end);
+        // the thresholds move only when a drain or a direct insert ran: most events only defer
+        // candidates, and skip the two cross-lane reads
+#ifdef LGX_TAU_EAGER  // development A/B (tools/score_lab_eager)
         if (SKIP) refresh_taus();
+        (void)tau_before;
+#else
+        if (SKIP && __ballot(st.tau != tau_before) != 0ull) refresh_taus();
+#endif
     };
     for (int64_t t = 0; t < ntiles; ++t) {
         LGX_STAT_T0

@@ -177,3 +177,20 @@ def test_c1_gowalla_shape_vs_oracle():
     ref = oracle.propagate(ip, ix, iv, E0.cpu().numpy(), cfg.K)
     err = np.abs(out - ref)
     assert (err <= 1e-5 * np.abs(ref) + 1e-6 * float(E0.abs().max())).all(), f"max err {err.max():.3e}"
+
+
+def test_c3_amazon_full_size_d128_vs_oracle():
+    """C3 (configs[2]: 52,643 x 91,599, 2,984,108 edges, K=4, d=128) at full size against the f64
+    oracle: fp32 storage at the north-star tolerance and bf16 storage (the config's dtype) at the
+    bf16 tolerance, from the same bf16-representable E0."""
+    cfg = CONFIGS["amazon"]
+    u, i = synth_edges(cfg, 2020, DEV)
+    A = lgx.build_norm_adj(u, i, cfg.n_users, cfg.n_items, dedup=True, device=DEV)
+    ip, ix, iv = A.indptr.cpu().numpy(), A.indices.cpu().numpy(), A.vals.cpu().numpy()
+    E0 = lgx.fill_normal((cfg.n_users + cfg.n_items, cfg.d), 0.1, 2020, device=DEV).to(torch.bfloat16)
+    ref = oracle.propagate(ip, ix, iv, E0.float().cpu().numpy(), cfg.K)
+    out32 = lgx.propagate(A, E0.float(), cfg.K).cpu().numpy()
+    err = np.abs(out32 - ref)
+    assert (err <= 1e-5 * np.abs(ref) + 1e-6 * float(E0.float().abs().max())).all(), f"fp32 max err {err.max():.3e}"
+    out16 = lgx.propagate(A, E0, cfg.K).cpu().numpy()
+    assert (np.abs(out16 - ref) <= 2e-2 * np.abs(ref) + 2e-2 * np.sqrt(np.mean(ref ** 2))).all()

@@ -69,35 +69,8 @@ int main(int argc, char** argv) {
     std::printf("LGX_MASK_ABL=%d\n", LGX_MASK_ABL);
     if (timeit("full", launch<0, 0>, true)) return 1;
 #else
-    {  // result check: the DMA variants must return the same lists
-        ScoreArgs a{Q, nullptr, items, B, I, d, nullptr, nullptr, k, p.n_splits, p.split_items,
-                    reinterpret_cast<float*>(ws),
-                    reinterpret_cast<int32_t*>(static_cast<char*>(ws) + (size_t)B * p.n_splits * k * 4), nullptr,
-                    nullptr};
-        const size_t n = (size_t)B * p.n_splits * k;
-        std::vector<int32_t> r0(n), r2(n);
-        if (launch<0, 0>(a, p, nullptr)) return 1;
-        HK(hipMemcpy(r0.data(), a.part_idx, n * 4, hipMemcpyDeviceToHost));
-        auto check = [&](const char* name, auto fn) -> int {
-            if (fn(a, p, nullptr)) return 1;
-            HK(hipMemcpy(r2.data(), a.part_idx, n * 4, hipMemcpyDeviceToHost));
-            size_t bad = 0;
-            for (size_t i = 0; i < n; ++i) bad += r0[i] != r2[i];
-            std::printf("%s vs all: %zu of %zu list entries differ\n", name, bad, n);
-            return 0;
-        };
-        if (check("dma by 4-7", launch<0, 2>)) return 1;
-        if (check("dma by 0-3", launch<0, 3>)) return 1;
-        if (check("dma by all (new path)", launch<0, 4>)) return 1;
-        if (check("dma all again", launch<0, 0>)) return 1;
-    }
-    if (timeit("full", launch<0, 0>, false)) return 1;
-    if (timeit("full dma by waves 4-7", launch<0, 2>, false)) return 1;
-    if (timeit("full dma by waves 4-7 no-stagger", launch<0, 2, true, false>, false)) return 1;
-    if (timeit("full dma by waves 4-7 regroup-always", launch<0, 2, false, true>, false)) return 1;
-    if (timeit("full no-stagger", launch<0, 0, true, false>, false)) return 1;
-    if (timeit("no-topk", launch<1, 0>, false)) return 1;
-    if (timeit("no-topk dma by waves 4-7", launch<1, 2>, false)) return 1;
+    for (int masked = 1; masked >= 0; --masked)
+        if (timeit("full", launch<0, 0>, masked)) return 1;
 #endif
     std::printf("done\n");
     return 0;
