@@ -197,7 +197,24 @@ def make_step(A, E0, K, d, dtype, world, cfg, rank, timings):
                                "floor": nnz * 8 + rows * d * es + Aop.n_cols * d * es, "hot_rows": 0, "hot_frac": 0.0}
             timings.append((e0, e1, models[key]))
 
+    def stack_fn(Aop, X, E0r, prev, out, n_mean):
+        if step.record:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        ops.propagate_layer_stack(Aop, X, E0r, prev, out, n_mean)
+        if step.record:
+            e1.record()
+            nnz, rows = Aop.nnz, Aop.n_rows
+            key = (id(Aop), _lib.LGX_LAYER_STACK)
+            if key not in models:
+                epi = epilogue_bytes(_lib.LGX_LAYER_STACK, rows, d, es, len(prev))
+                csr = nnz * 8 + 8 * (rows + 1)
+                models[key] = {"model": csr + epi + nnz * d * es, "gathered": csr + epi + nnz * d * es,
+                               "floor": nnz * 8 + rows * d * es + Aop.n_cols * d * es, "hot_rows": 0, "hot_frac": 0.0}
+            timings.append((e0, e1, models[key]))
+
     prop.layer_fn = layer_fn
+    prop.stack_fn = stack_fn
 
     def step(record):
         step.record = record

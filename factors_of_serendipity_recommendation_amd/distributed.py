@@ -135,18 +135,27 @@ def _default_epilogue_fn(y, mode, Y=None, E0=None, acc=None, out=None, n_mean=1.
     layer_epilogue(y, mode, Y=Y, E0=E0, acc=acc, out=out, n_mean=n_mean)
 
 
+def _default_stack_fn(A, X, E0, prev, out, n_mean):
+    from .ops import propagate_layer_stack
+    propagate_layer_stack(A, X, E0, prev, out, n_mean)
+
+
 class ShardedPropagation:
     """K-layer LightGCN propagation of a row-sharded graph (see module docstring)."""
 
     def __init__(self, shard: Shard, E0_user: torch.Tensor, E0_item: torch.Tensor, K: int,
-                 group=None, layer_fn: Optional[LayerFn] = None, epilogue_fn: Optional[LayerFn] = None):
+                 group=None, layer_fn: Optional[LayerFn] = None, epilogue_fn: Optional[LayerFn] = None,
+                 stack_fn: Optional[LayerFn] = None):
         """E0_user / E0_item: the FULL layer-0 tables in global row order (replicated input, as every
-        rank holds the embedding parameters); dtype f32 or bf16."""
+        rank holds the embedding parameters); dtype f32 or bf16.  The user side keeps its K-1 layer
+        tables and forms the mean in the last pull (stack_fn = lgx_propagate_layer_stack), as the
+        single-GPU lgx_propagate does; the item side keeps the f32 running sum of its own block."""
         self.s = shard
         self.K = K
         self.group = group
         self.layer_fn = layer_fn or _default_layer_fn
         self.epilogue_fn = epilogue_fn or _default_epilogue_fn
+        self.stack_fn = stack_fn or _default_stack_fn
         s = shard
         d = E0_user.shape[1]
         self.d = d
@@ -155,14 +164,13 @@ class ShardedPropagation:
         i0, i1 = int(s.item_bounds[s.rank]), int(s.item_bounds[s.rank + 1])
         self.E0u = E0_user[u0:u1].contiguous()
         self.E0i = E0_item[i0:i1].contiguous()
-        # users: local rows only, layer ping-pong; items: full padded tables, layer ping-pong
-        self.Xu = [self.E0u] + [torch.zeros((s.n_u_local, d), dtype=dt, device=dev) for _ in range(2)]
+        # users: local rows only, layers 0..K-1 kept; items: full padded tables, layer ping-pong
+        self.Xu = [self.E0u] + [torch.zeros((s.n_u_local, d), dtype=dt, device=dev) for _ in range(max(1, K - 1))]
         self.Xi = [pad_table(E0_item, s.item_bounds, s.mi)] + \
                   [torch.zeros((s.world * s.mi, d), dtype=dt, device=dev) for _ in range(2)]
         self.P = torch.zeros((s.world * s.mi, d), dtype=torch.float32, device=dev)  # push partials
         self.yi = torch.zeros((s.mi, d), dtype=torch.float32, device=dev)           # own item block sums
         self.send_i = torch.zeros((s.mi, d), dtype=dt, device=dev)
-        self.acc_u = torch.zeros((s.n_u_local, d), dtype=torch.float32, device=dev)
         self.acc_i = torch.zeros((s.n_i_local, d), dtype=torch.float32, device=dev)
         self.out_u = torch.zeros((s.n_u_local, d), dtype=torch.float32, device=dev)
         self.out_i = torch.zeros((s.n_i_local, d), dtype=torch.float32, device=dev)
@@ -215,14 +223,18 @@ class ShardedPropagation:
         for k in range(1, self.K + 1):
             mode = self._mode(k)
             # push: item partial sums from this rank's users at layer k-1
-            self.layer_fn(s.A_push, self.Xu[self._buf(k - 1)], _lib.LGX_LAYER_PARTIAL, out=self.P)
+            self.layer_fn(s.A_push, self.Xu[k - 1], _lib.LGX_LAYER_PARTIAL, out=self.P)
             rs = self._reduce_scatter()
             # pull: this rank's user rows from the full item table of layer k-1
             if ag is not None:
                 ag.wait()
-            Yu = self.Xu[self._buf(k)] if k < self.K else None
-            self.layer_fn(s.A_pull, self.Xi[self._buf(k - 1)], mode, Y=Yu, E0=self.E0u, acc=self.acc_u,
-                          out=self.out_u, n_mean=n_mean)
+            Xi = self.Xi[self._buf(k - 1)]
+            if self.K == 1:
+                self.layer_fn(s.A_pull, Xi, _lib.LGX_LAYER_ONLY, E0=self.E0u, out=self.out_u, n_mean=n_mean)
+            elif k < self.K:
+                self.layer_fn(s.A_pull, Xi, _lib.LGX_LAYER_PLAIN, Y=self.Xu[k])
+            else:
+                self.stack_fn(s.A_pull, Xi, self.E0u, self.Xu[1:self.K], self.out_u, n_mean)
             # items: epilogue on the summed block, then publish it for the next pull
             if rs is not None:
                 rs.wait()

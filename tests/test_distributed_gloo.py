@@ -39,6 +39,15 @@ def cpu_epilogue(y, mode, Y=None, E0=None, acc=None, out=None, n_mean=1.0):
         out.copy_((E0.float() + y) / n_mean)
 
 
+def cpu_stack(A, X, E0, prev, out, n_mean):
+    y = torch.from_numpy(oracle.spmm(A.indptr.numpy(), A.indices.numpy(), A.vals.numpy(),
+                                     X.float().numpy())).float()
+    acc = E0.float().clone()
+    for t in prev:
+        acc += t.float()
+    out.copy_((acc + y) / n_mean)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -60,7 +69,8 @@ def _worker(rank, world, port, K, result_q):
         A = CSRGraph(torch.from_numpy(ip), torch.from_numpy(ix), torch.from_numpy(iv), U + I, U + I, U, I)
         E0 = torch.from_numpy((rng.standard_normal((U + I, 8)) * 0.1).astype(np.float32))
         shard = make_shard(A, U, I, rank, world, seg_len=16)
-        prop = ShardedPropagation(shard, E0[:U], E0[U:], K, layer_fn=cpu_layer, epilogue_fn=cpu_epilogue)
+        prop = ShardedPropagation(shard, E0[:U], E0[U:], K, layer_fn=cpu_layer, epilogue_fn=cpu_epilogue,
+                                  stack_fn=cpu_stack)
         prop.step()
         prop.step()  # a second step must give the same answer (buffers re-used)
         ou, oi = prop.gather_outputs()
