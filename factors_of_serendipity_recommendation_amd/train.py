@@ -94,6 +94,7 @@ class _CapturedStep:
         self.n = torch.zeros(batch_size, dtype=torch.long, device=device)
         self.graph = None
         self.loss = None
+        self.failed = False
 
     def run(self, loss_class, u, p, n):
         self.u.copy_(u)
@@ -108,9 +109,16 @@ class _CapturedStep:
             with torch.cuda.stream(s):
                 out = loss_class.stageOne(self.u, self.p, self.n)
             torch.cuda.current_stream(dev).wait_stream(s)
-            self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
-                self.loss = loss_class.stageOne(self.u, self.p, self.n)
+            graph = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(graph):
+                    self.loss = loss_class.stageOne(self.u, self.p, self.n)
+            except RuntimeError as e:  # a model whose step cannot be captured: train eagerly
+                import warnings
+                warnings.warn(f"BPR step capture failed ({e}); training without the graph")
+                self.failed = True
+                return out
+            self.graph = graph
             return out
         self.graph.replay()
         return self.loss
@@ -156,7 +164,7 @@ def BPR_train_original(dataset, recommend_model, loss_class: BPRLoss, epoch: int
     try:
         for batch_i, i in enumerate(range(0, len(users), batch_size)):  # utils.minibatch
             u, p, n = users[i:i + batch_size], posItems[i:i + batch_size], negItems[i:i + batch_size]
-            if step is not None and u.numel() == batch_size:
+            if step is not None and not step.failed and u.numel() == batch_size:
                 cri = step.run(loss_class, u, p, n)
             else:
                 cri = loss_class.stageOne(u, p, n)
