@@ -778,6 +778,9 @@ __device__ __forceinline__ uint32_t lds_u32(const void* p) {
 // v_permlane16_swap per accumulator register then regroups them so that lane l holds 32 scores of
 // user l & 31 (items 16 q + 8 h + 0..7 of block q), the layout the top-k state expects: lanes l and
 // l + 32 still share a user.
+#ifndef LGX_DIRECT_EVENTS  // development A/B: -DLGX_DIRECT_EVENTS=0 keeps the regroup-always event path
+#define LGX_DIRECT_EVENTS 1
+#endif
 template <int KSTEPS, bool MINMAX, int ABLATE = 0, int WAVES = 8, int NACC = 2, bool STAGGER = true, bool M16 = true,
           int DMAPOS = 0, bool FASTSKIP = true>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
@@ -787,6 +790,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
     // l & 15 and 16 of user 16 + (l & 15)); the regroup into the top-k layout (16 v_permlane16_swap)
     // is paid only by tiles that have a survivor.  Min / max needs every score: not with MINMAX.
     constexpr bool SKIP = FASTSKIP && M16 && !MINMAX && ABLATE == 0;
+    constexpr bool DIRECT_EVENTS = LGX_DIRECT_EVENTS != 0;
     typedef LdsGeom<KSTEPS, WAVES, NACC> G;
     typedef Frag<LGX_DTYPE_BF16> F;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1025,6 +1029,40 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
                         m1 = fmaxf(m1, c[1][ib][r]);
                     }
                 if (__ballot((m0 >= tauA) | (m1 >= tauB)) == 0ull) return;  // wave-uniform fast path
+                // maxima of one item block's 4-score groups (both user blocks), re-derived on events
+                auto flagged = [&](int ib) {
+                    const float a0 = fmaxf(fmaxf(c[0][ib][0], c[0][ib][1]), fmaxf(c[0][ib][2], c[0][ib][3]));
+                    const float a1 = fmaxf(fmaxf(c[1][ib][0], c[1][ib][1]), fmaxf(c[1][ib][2], c[1][ib][3]));
+                    return __ballot((a0 >= tauA) | (a1 >= tauB)) != 0ull;
+                };
+                // Every list full (the sweep past its first tiles): defer the flagged item blocks'
+                // scores straight from the MFMA layout -- 4 v_permlane16_swap per block bring a
+                // user's 8 scores of that block to its own lanes -- instead of regrouping all 32
+                // scores and re-deriving the group maxima.  A lane whose slots would run over goes
+                // down the full path below, which re-appends from pcnt (the writes here only went
+                // to slots at or past it).
+                if (DIRECT_EVENTS && __ballot(st.len < st.k) == 0ull) {
+                    int n = st.pcnt;
+                    const uint32_t ibase = (uint32_t)(e0 + 8 * h);
+#pragma unroll
+                    for (int ib = 0; ib < 4; ++ib) {
+                        if (!flagged(ib)) continue;
+#pragma unroll
+                        for (int reg = 0; reg < 4; ++reg) {
+                            const auto sw = __builtin_amdgcn_permlane16_swap(
+                                __float_as_uint(c[0][ib][reg]), __float_as_uint(c[1][ib][reg]), false, false);
+                            const uint32_t it = ibase + 16 * ib + reg;
+                            st.pend[min(n, WaveTopK::kPend)] = ((uint64_t)it << 32) | sw[0];
+                            n += __uint_as_float(sw[0]) >= st.tau ? 1 : 0;
+                            st.pend[min(n, WaveTopK::kPend)] = ((uint64_t)(it + 4) << 32) | sw[1];
+                            n += __uint_as_float(sw[1]) >= st.tau ? 1 : 0;
+                        }
+                    }
+                    if (__ballot(n > WaveTopK::kPend) == 0ull) {
+                        st.pcnt = n;
+                        return;
+                    }
+                }
             }
             regroup();
         }
