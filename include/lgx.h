@@ -174,7 +174,9 @@ int lgx_propagate(const lgx_csr* A, const void* E0, float* out, int64_t d, int K
 int lgx_score_dense(const void* Q, const int64_t* user_rows, const void* items, int64_t B,
                     int64_t n_items, int64_t d, int dtype, int apply_sigmoid, float* scores,
                     lgx_stream_t stream);
-/* Workspace bytes of lgx_score_topk for this shape (item-split partial lists). */
+/* Workspace bytes of lgx_score_topk for this shape: the item-split partial lists, plus 24 parked
+ * keys per query half in full-sweep launches (candidates the mask's Bloom filter cannot rule out,
+ * settled by exact searches once, at the end of the sweep). */
 int lgx_score_topk_workspace(int64_t B, int64_t n_items, int k, size_t* ws_bytes);
 /*
  * Fused full-catalog scoring + positive mask + top-k; [B, n_items] is never materialised.
