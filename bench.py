@@ -47,8 +47,8 @@ sys.path.insert(0, ROOT)
 
 import factors_of_serendipity_recommendation_amd as lgx  # noqa: E402
 from factors_of_serendipity_recommendation_amd import _lib, ops  # noqa: E402
-from factors_of_serendipity_recommendation_amd.distributed import ShardedPropagation, make_shard  # noqa: E402
-from factors_of_serendipity_recommendation_amd.synth import CONFIGS, synth_graph  # noqa: E402
+from factors_of_serendipity_recommendation_amd.distributed import ShardedPropagation, make_shard_from_edges  # noqa: E402
+from factors_of_serendipity_recommendation_amd.synth import CONFIGS, synth_edges, synth_graph  # noqa: E402
 
 HBM_PEAK = 8.0e12        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BF16_MFMA_PEAK = 2.5e15  # dense bf16 MFMA spec
@@ -177,7 +177,8 @@ def make_step(A, E0, K, d, dtype, world, cfg, rank, timings):
                 if k < K:
                     X = bufs[k - 1]
         return step, A.nnz, A.n_rows
-    shard = make_shard(A, cfg.n_users, cfg.n_items, rank, world)
+    # N > 1: A is this rank's shard (built from the edge list, never the full operator)
+    shard = A
     prop = ShardedPropagation(shard, E0[:cfg.n_users], E0[cfg.n_users:], K)
     models = {}
 
@@ -428,8 +429,17 @@ def main():
     cfg = CONFIGS[args.config]
     main_dtype = torch.bfloat16 if (args.dtype or cfg.dtype) == "bf16" else torch.float32
     t0 = time.time()
-    A = synth_graph(cfg, seed=2020, device="cuda")
-    log(f"[bench] graph {cfg.name}: N={cfg.n_users + cfg.n_items} nnz={A.nnz} built in {time.time() - t0:.1f}s")
+    if world == 1:
+        A = synth_graph(cfg, seed=2020, device="cuda")
+        log(f"[bench] graph {cfg.name}: N={cfg.n_users + cfg.n_items} nnz={A.nnz} built in {time.time() - t0:.1f}s")
+    else:
+        # every rank draws the same seeded edge list and builds only its own rows
+        u, i = synth_edges(cfg, seed=2020, device="cuda")
+        A = make_shard_from_edges(u, i, cfg.n_users, cfg.n_items, rank, world)
+        del u, i
+        torch.cuda.empty_cache()
+        log(f"[bench] shard {rank}/{world} of {cfg.name}: {A.n_u_local} users, pull nnz {A.A_pull.nnz} "
+            f"built in {time.time() - t0:.1f}s")
     res = bench_propagation(args, rank, world, A, cfg, main_dtype, args.steps, args.warmup)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -96,3 +96,23 @@ def test_sharded_propagation_gloo(world, K):
         assert p.exitcode == 0
     assert eu < 1e-5 and ei < 1e-5, (eu, ei)
     assert len(sched) == 3 * K
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_shard_from_edges_equals_cut_of_full_operator(world):
+    """make_shard_from_edges (each rank builds only its rows from the sorted edge list) == make_shard
+    on the full oracle-built operator, bit for bit: bounds, indptr, column ids, values, transposes."""
+    from factors_of_serendipity_recommendation_amd.distributed import make_shard_from_edges
+    rng = np.random.default_rng(3)
+    U, I, E = 300, 200, 6000
+    keys = np.unique(rng.integers(0, U, E) * I + (rng.zipf(1.3, E) % I))
+    u, i = (keys // I).astype(np.int32), (keys % I).astype(np.int32)
+    ip, ix, iv = oracle.build_norm_adj(u, i, U, I, dedup=True)
+    A = CSRGraph(torch.from_numpy(ip), torch.from_numpy(ix), torch.from_numpy(iv), U + I, U + I, U, I)
+    for rank in range(world):
+        a = make_shard(A, U, I, rank, world, seg_len=16)
+        b = make_shard_from_edges(torch.from_numpy(u), torch.from_numpy(i), U, I, rank, world, seg_len=16)
+        assert np.array_equal(a.user_bounds, b.user_bounds) and a.mi == b.mi
+        for x, y in ((a.A_pull, b.A_pull), (a.A_push, b.A_push)):
+            assert torch.equal(x.indptr, y.indptr) and torch.equal(x.indices, y.indices)
+            assert torch.equal(x.vals, y.vals)
