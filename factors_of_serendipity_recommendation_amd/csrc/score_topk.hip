@@ -789,7 +789,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
     // SKIP: the fast-path test runs on the MFMA output layout itself (lane l holds 16 scores of user
     // l & 15 and 16 of user 16 + (l & 15)); the regroup into the top-k layout (16 v_permlane16_swap)
     // is paid only by tiles that have a survivor.  Min / max needs every score: not with MINMAX.
-    constexpr bool SKIP = FASTSKIP && M16 && !MINMAX && ABLATE == 0;
+    constexpr bool SKIP = FASTSKIP && M16 && !MINMAX && (ABLATE == 0 || ABLATE == 9);
     constexpr bool DIRECT_EVENTS = LGX_DIRECT_EVENTS != 0;
     typedef LdsGeom<KSTEPS, WAVES, NACC> G;
     typedef Frag<LGX_DTYPE_BF16> F;
@@ -902,7 +902,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
     wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(ahead, ntiles) - 1));
     __syncthreads();
     int buf = 0, sbuf = ahead;  // buffer of tile t / of tile t + ahead
-    const bool late = STAGGER && ABLATE == 0 && wave >= WAVES / 2;  // wave-uniform
+    const bool late = STAGGER && (ABLATE == 0 || ABLATE == 9) && wave >= WAVES / 2;  // wave-uniform
     f32x16 acc0, acc1;  // late waves: tile t-1's scores, held across the barrier
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     f32x4 c[2][4];      // 16x16x32 accumulators: c[ub][ib] = items 16 ib + 4 (lane >> 4) + reg, user 16 ub + (lane & 15)
@@ -914,6 +914,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
         tauB = __shfl(st.tau, 16 + (lane & 15));
     };
     if (SKIP) refresh_taus();
+    if (ABLATE == 9) tauA = tauB = __builtin_huge_valf();  // 9 (development): the fast path alone, no events
     // regroup: swap(X = user block 0, Y = user block 1) between rows 2m and 2m+1 (lanes l, l^16)
     // leaves X' = items 16 ib + 8 h + reg, Y' = items 16 ib + 8 h + 4 + reg of user l & 31
     auto regroup = [&]() {
@@ -966,7 +967,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
                         c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                             __builtin_bit_cast(bf16x8, fa[ib]), __builtin_bit_cast(bf16x8, uf[ub * KS2 + s2]),
                             c[ub][ib], 0, 0, 0);
-                    if (s2 + 1 < KS2) fa[ib] = frag(s2 + 1, ib);
+                    if (s2 + 1 < KS2 && ABLATE != 8) fa[ib] = frag(s2 + 1, ib);  // 8 (development): one read per tile
                 }
                 if (DMAPOS == 1 && s2 < G::PPW && refill) stage_piece(sbuf, refill_t0, s2);
             }
@@ -1081,7 +1082,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
     for (int64_t t = 0; t < ntiles; ++t) {
         LGX_STAT_T0
         const int64_t t0 = tile_start(t);
-        refill = ABLATE != 5 && ABLATE != 7 && t + ahead < ntiles;
+        refill = ABLATE != 5 && ABLATE != 7 && ABLATE != 8 && t + ahead < ntiles;
         if (refill) refill_t0 = tile_start(ABLATE == 6 ? 0 : t + ahead);  // 6 (development): L2-hot refills
         if (DMAPOS != 1 && refill) stage(sbuf, refill_t0);
 #ifdef LGX_SCORE_STATS
@@ -1095,7 +1096,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
 #ifdef LGX_SCORE_STATS
         const uint64_t stat_t1_ = __builtin_amdgcn_s_memtime();
 #endif
-        if (ABLATE == 1 || ABLATE == 5 || ABLATE == 6 || ABLATE == 7) {  // development: MFMA + LDS pipeline only (5: no refills either) (keeps the accumulators live)
+        if (ABLATE == 1 || ABLATE == 5 || ABLATE == 6 || ABLATE == 7 || ABLATE == 8) {  // development: MFMA + LDS pipeline only (5: no refills either) (keeps the accumulators live)
             float z = 0.0f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) z += acc0[r] + (NACC == 2 ? acc1[r] : 0.0f);
@@ -1119,7 +1120,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
         st.stat_[0] += 1;
 #endif
         // tiles t+2 .. t+ahead may stay in flight; tile t+1 must have landed
-        if (ABLATE != 7) {  // 7 (development): no refills and no barrier -- the MFMA + LDS-read ceiling
+        if (ABLATE != 7 && ABLATE != 8) {  // 7 (development): no refills and no barrier -- the MFMA + LDS-read ceiling
             wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(t + ahead, ntiles - 1) - (t + 1)));
             __syncthreads();
         }

@@ -69,8 +69,17 @@ int main(int argc, char** argv) {
     std::printf("LGX_MASK_ABL=%d\n", LGX_MASK_ABL);
     if (timeit("full", launch<0, 0>, true)) return 1;
 #else
-    for (int masked = 1; masked >= 0; --masked)
-        if (timeit("full", launch<0, 0>, masked)) return 1;
+    if (getenv("LAB_ABL")) {  // the MFMA / LDS-read / refill ladder (unmasked)
+        if (timeit("full", launch<0, 0>, false)) return 1;
+        if (timeit("no-topk", launch<1, 0>, false)) return 1;
+        if (timeit("fast path only (no events)", launch<9, 0>, false)) return 1;
+        if (timeit("no-topk no-refill", launch<5, 0>, false)) return 1;
+        if (timeit("no-topk no-refill no-barrier", launch<7, 0>, false)) return 1;
+        if (timeit("... one fragment read per tile", launch<8, 0>, false)) return 1;
+    } else {
+        for (int masked = 1; masked >= 0; --masked)
+            if (timeit("full", launch<0, 0>, masked)) return 1;
+    }
 #endif
     std::printf("done\n");
     return 0;
