@@ -114,6 +114,11 @@ struct ScoreArgs {
     int32_t* part_idx;    // [B, n_splits, k]
     uint32_t* minmax;     // ordered {min, max} or nullptr
     uint64_t* susp;       // [B, 2, kSuspSlots] parked keys (LDS kernel, full sweep), or nullptr
+    // seeded sweep (LDS kernel, full sweep): each user's exact top-k over items [0, seed_items),
+    // [B, k] (index -1 = empty); the sweep then covers [seed_items, n_items) only
+    const float* seed_score;
+    const int32_t* seed_idx;
+    int64_t seed_items;
 };
 
 // Candidates whose mask test the Bloom filter cannot settle ("suspects", ~10 % of the survivors) are
@@ -266,6 +271,24 @@ struct WaveTopK {
         mn = INFINITY;
         mx = -INFINITY;
         park = false;
+    }
+    // the list starts as the user's top-k over the seed items (already mask-filtered, so the keys go
+    // in without tests); both lane halves read the same entries and hold the same {len, mp, kmin}
+    __device__ __forceinline__ void seed(const ScoreArgs& a) {
+        if (!user_ok) return;
+        const float* ss = a.seed_score + (size_t)b * k;
+        const int32_t* si = a.seed_idx + (size_t)b * k;
+        int n = 0;
+        for (int j = 0; j < k; ++j) {
+            const int32_t it = si[j];
+            if (it < 0) continue;
+            if (h == 0) keys[n] = make_key(ss[j], it);
+            ++n;
+        }
+        __builtin_amdgcn_wave_barrier();  // half 0's list writes precede half 1's reads
+        len = n;
+        if (len == k) rescan();
+        refresh_tau();
     }
     // full-sweep launches only (one workgroup per user); split lists test at once
     __device__ __forceinline__ void enable_suspects(const ScoreArgs& a) {
@@ -839,6 +862,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
     st.init(lk, lk + list_keys_per_wave(k), k, lane, b, user_ok);
     st.enable_suspects(a);
     st.build_bloom(a);
+    if (a.seed_score) st.seed(a);
     // consume the prologue loads here: otherwise the compiler treats them as possibly pending at
     // the loop header and waits vmcnt(0) -- i.e. for the tile prefetch -- in every iteration
 #pragma unroll
@@ -850,7 +874,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
 #pragma unroll
     for (int w = 0; w < kBloomWords; ++w) asm volatile("" : "+v"(st.bl[w]));
 
-    const int64_t i_begin = (int64_t)split * a.split_items;
+    const int64_t i_begin = a.seed_items + (int64_t)split * a.split_items;
     const int64_t i_end = min(a.n_items, i_begin + a.split_items);
     const int64_t ntiles = i_end > i_begin ? (i_end - i_begin + G::TILE_ITEMS - 1) / G::TILE_ITEMS : 0;
     // single split: every workgroup sweeps the whole catalog, starting at a rotation shared by the
@@ -1735,6 +1759,16 @@ int plan_ranges(int64_t B, int64_t n_items, int dtype, int64_t d, int k, UserRan
     return n;
 }
 
+// Seeded full sweeps: the first kSeedItems items get a launch of their own, whose lists (written to
+// the split-list workspace) seed the sweep over the rest, which reads and overwrites them in place.
+// Exact either way (same kernel, same scores, the lists are sets); the event-dense start of the sweep
+// and its quiet remainder then run as two launches.  Lab, 131 072 users x 1M items (masked /
+// unmasked): one sweep 59.9 / 56.4 ms, seeded 58.1 / 55.7 ms (profiles/r02_score_lab_seeded.txt).
+constexpr int64_t kSeedItems = 65536;
+inline bool seeded_sweep(const SplitPlan& p, bool minmax, int64_t n_items) {
+    return p.lds && p.n_splits == 1 && !minmax && n_items >= 4 * kSeedItems;
+}
+
 size_t topk_ws_bytes(int64_t B, int64_t n_items, int k, int dtype, int64_t d) {
     UserRange r[2];
     const int n = plan_ranges(B, n_items, dtype, d, k, r);
@@ -1771,8 +1805,9 @@ extern "C" int lgx_score_topk_plan(int64_t B, int64_t n_items, int64_t d, int dt
                                  : (v1_waves(k) == 4 ? "score_topk_kernel<4 waves>" : "score_topk_kernel<1 wave>");
         const char* mode = p.lds ? (p.n_splits == 1 ? "full-sweep" : (p.xcd_affine ? "split-xcd" : "split"))
                                  : "split";
-        off += snprintf(buf + off, len - off, "%s%s users[%lld,%lld) %s n_splits=%d utiles=%lld",
-                        i ? "; " : "", kern, (long long)r[i].u0, (long long)r[i].u1, mode, p.n_splits,
+        off += snprintf(buf + off, len - off, "%s%s users[%lld,%lld) %s%s n_splits=%d utiles=%lld",
+                        i ? "; " : "", kern, (long long)r[i].u0, (long long)r[i].u1, mode,
+                        seeded_sweep(p, false, n_items) ? " (seeded by items [0,65536))" : "", p.n_splits,
                         (long long)p.n_utiles);
     }
     return LGX_OK;
@@ -1837,7 +1872,18 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
         else if (p.lds && ablate5) rc = launch_lds<false, 5>(a, p, stream);
         else
 #endif
-        if (p.lds) rc = mm ? launch_lds<true>(a, p, stream) : launch_lds<false>(a, p, stream);
+        if (seeded_sweep(p, mm, n_items)) {
+            ScoreArgs pre = a;
+            pre.n_items = kSeedItems;
+            pre.split_items = kSeedItems;
+            rc = launch_lds<false>(pre, p, stream);
+            if (rc) return rc;
+            a.seed_score = a.part_score;
+            a.seed_idx = a.part_idx;
+            a.seed_items = kSeedItems;
+            a.split_items = n_items - kSeedItems;
+            rc = launch_lds<false>(a, p, stream);
+        } else if (p.lds) rc = mm ? launch_lds<true>(a, p, stream) : launch_lds<false>(a, p, stream);
         else if (dtype == LGX_DTYPE_F32) rc = mm ? launch_v1<LGX_DTYPE_F32, true>(a, kch, stream)
                                                  : launch_v1<LGX_DTYPE_F32, false>(a, kch, stream);
         else rc = mm ? launch_v1<LGX_DTYPE_BF16, true>(a, kch, stream)

@@ -93,7 +93,9 @@ def test_c5_scoring_full_sweep_plan_d256():
     catalog-split launch for the 67-tile remainder) at d=256 bf16 with the train mask."""
     B, I, d, k = 256 * (256 + 67), 100_000, 256, 20
     plan = ops.score_topk_plan(B, I, d, torch.bfloat16, k)
-    bench = ops.score_topk_plan(1_000_000, 1_000_000, d, torch.bfloat16, k)
+    # the bench's 1M-item catalog seeds its full sweep (test_seeded_full_sweep_equals_one_sweep)
+    bench = ops.score_topk_plan(1_000_000, 1_000_000, d, torch.bfloat16, k).replace(
+        " (seeded by items [0,65536))", "")
     kinds = [p.split(" users")[0] + " " + p.split(") ")[1].split(" n_splits")[0] for p in plan.split("; ")]
     bkinds = [p.split(" users")[0] + " " + p.split(") ")[1].split(" n_splits")[0] for p in bench.split("; ")]
     assert kinds == bkinds and "full-sweep" in plan and len(kinds) == 2, (plan, bench)
@@ -162,6 +164,43 @@ def test_full_sweep_masks_on_the_top_items(n_top, n_rand):
     srt = got_idx.sort(1).values
     assert (srt[:, 1:] != srt[:, :-1]).all()
     assert torch.allclose(val[sel].double(), got, rtol=1e-5, atol=1e-5)
+
+
+def test_seeded_full_sweep_equals_one_sweep():
+    """Catalogs of >= 262 144 items run the full sweep as two launches: items [0, 65536) first, whose
+    lists seed the sweep over the rest.  Masks put every user's own best seed-range items (and random
+    ones on both sides of the cut) out of play.  The lists must equal, as sets, the one-launch sweep
+    (the min/max variant never seeds) and the float64 top-k of the unmasked items."""
+    B, I, d, k = 256 * 256, 300_000, 256, 20
+    plan = ops.score_topk_plan(B, I, d, torch.bfloat16, k)
+    assert "full-sweep (seeded by items [0,65536))" in plan, plan
+    g = torch.Generator(device=DEV).manual_seed(29)
+    Q = (torch.randn(B, d, device=DEV, generator=g) / 16).bfloat16()
+    items = (torch.randn(I, d, device=DEV, generator=g) / 16).bfloat16()
+    tops = []
+    for u0 in range(0, B, 8192):
+        s = Q[u0:u0 + 8192].float() @ items[:65536].float().T
+        tops.append(torch.topk(s, 8, dim=1).indices)
+    m = torch.cat([torch.cat(tops), torch.randint(0, I, (B, 40), device=DEV, generator=g)], 1).sort(1).values
+    keep = torch.ones_like(m, dtype=torch.bool)
+    keep[:, 1:] = m[:, 1:] != m[:, :-1]
+    indptr = torch.zeros(B + 1, dtype=torch.int64, device=DEV)
+    indptr[1:] = torch.cumsum(keep.sum(1), 0)
+    mask = (indptr, m[keep].to(torch.int32))
+    idx, val = lgx.score_topk(Q, items, k, mask=mask)
+    idx1, val1, _ = lgx.score_topk(Q, items, k, mask=mask, want_minmax=True)
+    ka = torch.sort(idx.long(), 1)
+    kb = torch.sort(idx1.long(), 1)
+    assert torch.equal(ka.values, kb.values), "seeded lists differ from the one-launch sweep"
+    assert torch.equal(val.gather(1, ka.indices), val1.gather(1, kb.indices))
+    sel = torch.randint(0, B, (1500,), device=DEV, generator=g)
+    S = Q[sel].double() @ items.double().T
+    for j, u in enumerate(sel.tolist()):
+        S[j, mask[1][indptr[u]:indptr[u + 1]].long()] = float("-inf")
+    kth = torch.topk(S, k, dim=1).values[:, -1:]
+    got = S.gather(1, idx[sel].long())
+    assert torch.isfinite(got).all(), "a masked item was returned"
+    assert (got >= kth - 1e-5 * kth.abs().clamp(min=1.0)).all()
 
 
 def test_c1_gowalla_shape_vs_oracle():

@@ -69,7 +69,62 @@ int main(int argc, char** argv) {
     std::printf("LGX_MASK_ABL=%d\n", LGX_MASK_ABL);
     if (timeit("full", launch<0, 0>, true)) return 1;
 #else
-    if (getenv("LAB_ABL")) {  // the MFMA / LDS-read / refill ladder (unmasked)
+    if (getenv("LAB_SEED")) {  // seeded sweep: exact top-k over items [0, S) first, then [S, I)
+        const int64_t S = std::atoll(getenv("LAB_SEED"));
+        const int masked = getenv("LAB_UNMASKED") ? 0 : 1;
+        const int64_t* mp_ = masked ? mp : nullptr;
+        const int32_t* mi_ = masked ? mi : nullptr;
+        const size_t lk = (size_t)B * k;
+        float *sv, *fv;
+        int32_t *si, *fi;
+        HK(hipMalloc(&sv, lk * 4));
+        HK(hipMalloc(&si, lk * 4));
+        HK(hipMalloc(&fv, lk * 4));
+        HK(hipMalloc(&fi, lk * 4));
+        uint64_t* susp = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + (size_t)B * p.n_splits * k * 8);
+        ScoreArgs full{Q, nullptr, items, B, I, d, mp_, mi_, k, 1, I, fv, fi, nullptr, susp};
+        ScoreArgs pre{Q, nullptr, items, B, S, d, mp_, mi_, k, 1, S, sv, si, nullptr, susp};
+        ScoreArgs main_{Q, nullptr, items, B, I, d, mp_, mi_, k, 1, I - S, reinterpret_cast<float*>(ws),
+                        reinterpret_cast<int32_t*>(static_cast<char*>(ws) + lk * 4), nullptr, susp, sv, si, S};
+        SplitPlan q = p;
+        q.n_splits = 1;
+        auto run = [&](const ScoreArgs& x) { return launch<0, 0>(x, q, nullptr); };
+        float t[3] = {1e30f, 1e30f, 1e30f};
+        for (int r = 0; r < 3; ++r) {
+            const ScoreArgs* xs[3] = {&full, &pre, &main_};
+            for (int v = 0; v < 3; ++v) {
+                HK(hipEventRecord(e0, nullptr));
+                if (run(*xs[v])) { std::printf("launch failed: %s\n", lgx_last_error()); return 1; }
+                HK(hipEventRecord(e1, nullptr));
+                HK(hipEventSynchronize(e1));
+                float ms;
+                HK(hipEventElapsedTime(&ms, e0, e1));
+                t[v] = std::min(t[v], ms);
+            }
+        }
+        const double fl = 2.0 * B * I * d;
+        std::printf("masked=%d S=%lld: full %.2f ms (%.0f TF/s) | pre [0,S) %.2f ms | seeded [S,I) %.2f ms (%.0f TF/s over I) | pre+seeded %.2f ms\n",
+                    masked, (long long)S, t[0], fl / (t[0] * 1e-3) / 1e12, t[1], t[2], fl / (t[2] * 1e-3) / 1e12, t[1] + t[2]);
+        // the seeded lists must equal the one-sweep lists as (score, index) sets
+        std::vector<float> a1(lk), a2(lk);
+        std::vector<int32_t> b1(lk), b2(lk);
+        HK(hipMemcpy(a1.data(), fv, lk * 4, hipMemcpyDeviceToHost));
+        HK(hipMemcpy(b1.data(), fi, lk * 4, hipMemcpyDeviceToHost));
+        HK(hipMemcpy(a2.data(), ws, lk * 4, hipMemcpyDeviceToHost));
+        HK(hipMemcpy(b2.data(), static_cast<char*>(ws) + lk * 4, lk * 4, hipMemcpyDeviceToHost));
+        int64_t bad = 0;
+        for (int64_t u = 0; u < B; ++u) {
+            std::vector<std::pair<int32_t, float>> x, y;
+            for (int j = 0; j < k; ++j) {
+                x.push_back({b1[u * k + j], a1[u * k + j]});
+                y.push_back({b2[u * k + j], a2[u * k + j]});
+            }
+            std::sort(x.begin(), x.end());
+            std::sort(y.begin(), y.end());
+            if (x != y) ++bad;
+        }
+        std::printf("seeded vs one sweep: %lld of %lld users differ\n", (long long)bad, (long long)B);
+    } else if (getenv("LAB_ABL")) {  // the MFMA / LDS-read / refill ladder (unmasked)
         if (timeit("full", launch<0, 0>, false)) return 1;
         if (timeit("no-topk", launch<1, 0>, false)) return 1;
         if (timeit("fast path only (no events)", launch<9, 0>, false)) return 1;
