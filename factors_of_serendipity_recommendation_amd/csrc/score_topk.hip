@@ -1759,14 +1759,15 @@ int plan_ranges(int64_t B, int64_t n_items, int dtype, int64_t d, int k, UserRan
     return n;
 }
 
-// Seeded full sweeps: the first kSeedItems items get a launch of their own, whose lists (written to
-// the split-list workspace) seed the sweep over the rest, which reads and overwrites them in place.
-// Exact either way (same kernel, same scores, the lists are sets); the event-dense start of the sweep
-// and its quiet remainder then run as two launches.  Lab, 131 072 users x 1M items (masked /
-// unmasked): one sweep 59.9 / 56.4 ms, seeded 58.1 / 55.7 ms (profiles/r02_score_lab_seeded.txt).
-constexpr int64_t kSeedItems = 65536;
+// Seeded full sweeps: the catalog is swept in stages [0, 16384), [16384, 131072), ... (x8 while the
+// stage end is at most half the catalog), then the rest; each stage is a launch of its own whose
+// lists (the split-list workspace) seed the next, which reads and overwrites them in place.  Exact
+// (same kernel, same scores, the lists are sets); the event-dense start of the sweep runs apart from
+// its quiet remainder.  Lab, 983 040 users x 1M items, masked, one box: one sweep 458.4 ms, two
+// stages (65536) 449.5, three (16384, 131072) 444.9 (profiles/r02_score_lab_seeded.txt).
+constexpr int64_t kSeedItems = 16384;
 inline bool seeded_sweep(const SplitPlan& p, bool minmax, int64_t n_items) {
-    return p.lds && p.n_splits == 1 && !minmax && n_items >= 4 * kSeedItems;
+    return p.lds && p.n_splits == 1 && !minmax && n_items >= 16 * kSeedItems;
 }
 
 size_t topk_ws_bytes(int64_t B, int64_t n_items, int k, int dtype, int64_t d) {
@@ -1807,7 +1808,7 @@ extern "C" int lgx_score_topk_plan(int64_t B, int64_t n_items, int64_t d, int dt
                                  : "split";
         off += snprintf(buf + off, len - off, "%s%s users[%lld,%lld) %s%s n_splits=%d utiles=%lld",
                         i ? "; " : "", kern, (long long)r[i].u0, (long long)r[i].u1, mode,
-                        seeded_sweep(p, false, n_items) ? " (seeded by items [0,65536))" : "", p.n_splits,
+                        seeded_sweep(p, false, n_items) ? " (seeded in stages)" : "", p.n_splits,
                         (long long)p.n_utiles);
     }
     return LGX_OK;
@@ -1873,16 +1874,19 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
         else
 #endif
         if (seeded_sweep(p, mm, n_items)) {
-            ScoreArgs pre = a;
-            pre.n_items = kSeedItems;
-            pre.split_items = kSeedItems;
-            rc = launch_lds<false>(pre, p, stream);
-            if (rc) return rc;
-            a.seed_score = a.part_score;
-            a.seed_idx = a.part_idx;
-            a.seed_items = kSeedItems;
-            a.split_items = n_items - kSeedItems;
-            rc = launch_lds<false>(a, p, stream);
+            rc = LGX_OK;
+            for (int64_t lo = 0, hi = kSeedItems; lo < n_items && rc == LGX_OK; lo = hi, hi *= 8) {
+                ScoreArgs st = a;
+                st.n_items = 2 * hi <= n_items ? hi : n_items;
+                st.seed_items = lo;
+                st.split_items = st.n_items - lo;
+                if (lo > 0) {
+                    st.seed_score = a.part_score;
+                    st.seed_idx = a.part_idx;
+                }
+                rc = launch_lds<false>(st, p, stream);
+                if (st.n_items == n_items) break;
+            }
         } else if (p.lds) rc = mm ? launch_lds<true>(a, p, stream) : launch_lds<false>(a, p, stream);
         else if (dtype == LGX_DTYPE_F32) rc = mm ? launch_v1<LGX_DTYPE_F32, true>(a, kch, stream)
                                                  : launch_v1<LGX_DTYPE_F32, false>(a, kch, stream);

@@ -94,8 +94,7 @@ def test_c5_scoring_full_sweep_plan_d256():
     B, I, d, k = 256 * (256 + 67), 100_000, 256, 20
     plan = ops.score_topk_plan(B, I, d, torch.bfloat16, k)
     # the bench's 1M-item catalog seeds its full sweep (test_seeded_full_sweep_equals_one_sweep)
-    bench = ops.score_topk_plan(1_000_000, 1_000_000, d, torch.bfloat16, k).replace(
-        " (seeded by items [0,65536))", "")
+    bench = ops.score_topk_plan(1_000_000, 1_000_000, d, torch.bfloat16, k).replace(" (seeded in stages)", "")
     kinds = [p.split(" users")[0] + " " + p.split(") ")[1].split(" n_splits")[0] for p in plan.split("; ")]
     bkinds = [p.split(" users")[0] + " " + p.split(") ")[1].split(" n_splits")[0] for p in bench.split("; ")]
     assert kinds == bkinds and "full-sweep" in plan and len(kinds) == 2, (plan, bench)
@@ -167,19 +166,19 @@ def test_full_sweep_masks_on_the_top_items(n_top, n_rand):
 
 
 def test_seeded_full_sweep_equals_one_sweep():
-    """Catalogs of >= 262 144 items run the full sweep as two launches: items [0, 65536) first, whose
-    lists seed the sweep over the rest.  Masks put every user's own best seed-range items (and random
-    ones on both sides of the cut) out of play.  The lists must equal, as sets, the one-launch sweep
+    """Catalogs of >= 262 144 items run the full sweep in stages ([0, 16384), [16384, 131072), the
+    rest), each seeding the next.  Masks put every user's own best first-stage items (and random
+    ones everywhere) out of play.  The lists must equal, as sets, the one-launch sweep
     (the min/max variant never seeds) and the float64 top-k of the unmasked items."""
     B, I, d, k = 256 * 256, 300_000, 256, 20
     plan = ops.score_topk_plan(B, I, d, torch.bfloat16, k)
-    assert "full-sweep (seeded by items [0,65536))" in plan, plan
+    assert "full-sweep (seeded in stages)" in plan, plan
     g = torch.Generator(device=DEV).manual_seed(29)
     Q = (torch.randn(B, d, device=DEV, generator=g) / 16).bfloat16()
     items = (torch.randn(I, d, device=DEV, generator=g) / 16).bfloat16()
     tops = []
     for u0 in range(0, B, 8192):
-        s = Q[u0:u0 + 8192].float() @ items[:65536].float().T
+        s = Q[u0:u0 + 8192].float() @ items[:16384].float().T
         tops.append(torch.topk(s, 8, dim=1).indices)
     m = torch.cat([torch.cat(tops), torch.randint(0, I, (B, 40), device=DEV, generator=g)], 1).sort(1).values
     keep = torch.ones_like(m, dtype=torch.bool)

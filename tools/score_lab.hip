@@ -124,6 +124,49 @@ int main(int argc, char** argv) {
             if (x != y) ++bad;
         }
         std::printf("seeded vs one sweep: %lld of %lld users differ\n", (long long)bad, (long long)B);
+        if (getenv("LAB_SEED1")) {  // three stages: [0, S1), [S1, S), [S, I), each seeding the next
+            const int64_t S1 = std::atoll(getenv("LAB_SEED1"));
+            ScoreArgs s0{Q, nullptr, items, B, S1, d, mp_, mi_, k, 1, S1, main_.part_score, main_.part_idx, nullptr, susp};
+            ScoreArgs s1{Q, nullptr, items, B, S, d, mp_, mi_, k, 1, S - S1, main_.part_score, main_.part_idx, nullptr, susp,
+                         main_.part_score, main_.part_idx, S1};
+            ScoreArgs s2 = main_;
+            s2.seed_score = main_.part_score;
+            s2.seed_idx = main_.part_idx;
+            float u[3] = {1e30f, 1e30f, 1e30f};
+            for (int r = 0; r < 3; ++r) {
+                const ScoreArgs* xs[3] = {&s0, &s1, &s2};
+                for (int v = 0; v < 3; ++v) {
+                    HK(hipEventRecord(e0, nullptr));
+                    if (run(*xs[v])) return 1;
+                    HK(hipEventRecord(e1, nullptr));
+                    HK(hipEventSynchronize(e1));
+                    float ms;
+                    HK(hipEventElapsedTime(&ms, e0, e1));
+                    u[v] = std::min(u[v], ms);
+                }
+            }
+            // the timed repetitions re-seed from lists already past [S1, I): rerun the chain once for the check
+            for (int v = 0; v < 3; ++v) {
+                const ScoreArgs* xs[3] = {&s0, &s1, &s2};
+                if (run(*xs[v])) return 1;
+            }
+            HK(hipDeviceSynchronize());
+            HK(hipMemcpy(a2.data(), ws, lk * 4, hipMemcpyDeviceToHost));
+            HK(hipMemcpy(b2.data(), static_cast<char*>(ws) + lk * 4, lk * 4, hipMemcpyDeviceToHost));
+            bad = 0;
+            for (int64_t uu = 0; uu < B; ++uu) {
+                std::vector<std::pair<int32_t, float>> x, y;
+                for (int j = 0; j < k; ++j) {
+                    x.push_back({b1[uu * k + j], a1[uu * k + j]});
+                    y.push_back({b2[uu * k + j], a2[uu * k + j]});
+                }
+                std::sort(x.begin(), x.end());
+                std::sort(y.begin(), y.end());
+                if (x != y) ++bad;
+            }
+            std::printf("3 stages S1=%lld S=%lld: %.2f + %.2f + %.2f = %.2f ms; %lld users differ\n", (long long)S1,
+                        (long long)S, u[0], u[1], u[2], u[0] + u[1] + u[2], (long long)bad);
+        }
     } else if (getenv("LAB_ABL")) {  // the MFMA / LDS-read / refill ladder (unmasked)
         if (timeit("full", launch<0, 0>, false)) return 1;
         if (timeit("no-topk", launch<1, 0>, false)) return 1;
