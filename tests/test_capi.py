@@ -119,3 +119,16 @@ def test_strat_thresholds_reproduce_float16_labels(mn, mx, num_fold):
     ref = np.clip(np.nan_to_num(q, nan=num_fold, posinf=num_fold, neginf=0), 0, num_fold).astype(np.int64)
     got = (s[:, None] >= t[None, :]).sum(1)
     assert np.array_equal(got, ref)
+
+
+def test_score_topk_plan_seeds_large_full_sweeps():
+    """Host only (lgx_score_topk_plan): the full-sweep LDS plan is swept in seeded stages once the
+    catalog reaches 262 144 items; smaller catalogs and catalog-split launches run as one launch."""
+    import torch
+    from factors_of_serendipity_recommendation_amd import ops
+    big = ops.score_topk_plan(1_000_000, 1_000_000, 256, torch.bfloat16, 20)
+    assert big.split("; ")[0].endswith("full-sweep (seeded in stages) n_splits=1 utiles=3840"), big
+    assert "seeded" not in big.split("; ")[1]
+    assert "seeded" in ops.score_topk_plan(65536, 262_144, 256, torch.bfloat16, 20)
+    assert "seeded" not in ops.score_topk_plan(65536, 262_143, 256, torch.bfloat16, 20)
+    assert "seeded" not in ops.score_topk_plan(4096, 1_000_000, 256, torch.bfloat16, 20)
