@@ -85,10 +85,12 @@ def lib_sha() -> str:
     return h.hexdigest()[:16]
 
 
-def measured_traffic(config: str, dtype: str, world: int, kernels) -> tuple:
+def measured_traffic(config: str, dtype: str, world: int, kernels, calls_from=None) -> tuple:
     """Calibrated counter bytes per launch from the newest committed PMC summary of this workload
     (profiles/rNN_<config>_pmc_traffic.json), if it was collected from the library build that is
-    running now.  Returns (GB per launch or None, source or reason)."""
+    running now.  Returns (GB per launch or None, source or reason).  calls_from = (kernel, its
+    dispatches per call): the bytes of every dispatch of `kernels` per library call instead (a call
+    that launches a kernel several times, as lgx_score_topk's seeded stages do)."""
     import glob
     if world != 1:
         return None, "PMC profiles are single-GPU"
@@ -100,7 +102,12 @@ def measured_traffic(config: str, dtype: str, world: int, kernels) -> tuple:
     if doc.get("lib_sha256_16") != lib_sha():
         return None, f"{src} was taken from another liblgx.so build"
     try:
-        b = sum(doc["kernels"][dtype][k]["hbm_bytes_per_launch"] for k in kernels)
+        ks = doc["kernels"][dtype]
+        if calls_from:
+            calls = ks[calls_from[0]]["dispatches"] / calls_from[1]
+            b = sum(ks[k]["hbm_bytes_per_launch"] * ks[k]["dispatches"] for k in kernels) / calls
+        else:
+            b = sum(ks[k]["hbm_bytes_per_launch"] for k in kernels)
     except KeyError:
         return None, f"{src} has no {dtype} entry"
     return b / 1e9, src
@@ -354,17 +361,21 @@ def bench_scoring(args, rank, world):
     elapsed = max_over_ranks(time.perf_counter() - t_start, world)
     mean_launch = float(np.mean([a.elapsed_time(b) for a, b in ev])) / 1e3
     flops = 2.0 * B * n_items * d
-    traffic, tsrc = measured_traffic(args.config, "scoring", world, ["score_topk_bf16_lds"])
+    plan = ops.score_topk_plan(B, n_items, d, torch.bfloat16, k)
+    # per lgx_score_topk call: every stage of every user range (finalize runs once per range)
+    traffic, tsrc = measured_traffic(args.config, "scoring", world, ["score_topk_bf16_lds", "score_topk_finalize"],
+                                     calls_from=("score_topk_finalize", plan.count("; ") + 1))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = scoring_cpu_baseline(Q, items, pos, k, args.cpu_score_users)
     return {"value": B_total * n_items * steps / elapsed, "unit": "items/s", "users_per_step": B_total,
             "n_items": n_items, "d": d, "k": k, "dtype": "bf16", "ms_per_step": elapsed / steps * 1e3,
-            "plan": ops.score_topk_plan(B, n_items, d, torch.bfloat16, k),
+            "plan": plan,
             "roofline": {"bound": "mfma", "achieved": flops / mean_launch / 1e12, "peak": BF16_MFMA_PEAK / 1e12,
                          "unit": "TFLOP/s", "frac": flops / mean_launch / BF16_MFMA_PEAK, "traffic": traffic,
-                         "traffic_unit": "GB/launch", "traffic_source": tsrc,
-                         "kernel": "score_topk_bf16_lds (+ score_topk_finalize, both inside the timed launch)"},
+                         "traffic_unit": "GB/call", "traffic_source": tsrc,
+                         "kernel": "score_topk_bf16_lds (+ score_topk_finalize, both inside the timed launch)",
+                         "launch": "one lgx_score_topk call: its seeded stages and split tail"},
             "cpu_baseline": cpu}
 
 
