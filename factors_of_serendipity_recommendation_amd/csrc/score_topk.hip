@@ -1759,12 +1759,14 @@ int plan_ranges(int64_t B, int64_t n_items, int dtype, int64_t d, int k, UserRan
     return n;
 }
 
-// Seeded full sweeps: the catalog is swept in stages [0, 16384), [16384, 131072), ... (x8 while the
-// stage end is at most half the catalog), then the rest; each stage is a launch of its own whose
+// Seeded full sweeps: the catalog is swept in stages [0, 16384), [16384, 32768), ... (doubling while
+// a stage ends before 2/3 of the catalog), then the rest; each stage is a launch of its own whose
 // lists (the split-list workspace) seed the next, which reads and overwrites them in place.  Exact
-// (same kernel, same scores, the lists are sets); the event-dense start of the sweep runs apart from
-// its quiet remainder.  Lab, 983 040 users x 1M items, masked, one box: one sweep 458.4 ms, two
-// stages (65536) 449.5, three (16384, 131072) 444.9 (profiles/r02_score_lab_seeded.txt).
+// (same kernel, same scores, the lists are sets).  The event-dense start of the sweep runs apart from
+// its quiet remainder, and every stage restarts the co-resident workgroups of an XCD on the same
+// tile, so their drift (and L2 misses) stays bounded.  Lab, 983 040 users x 1M items, masked: one
+// sweep 463.7 ms, these 7 stages 431.9 ms (-6.9 %); 2 stages -2 %, 3 stages -4 %
+// (profiles/r02_score_lab_seeded.txt, profiles/r02_score_lab_stages.txt).
 constexpr int64_t kSeedItems = 16384;
 inline bool seeded_sweep(const SplitPlan& p, bool minmax, int64_t n_items) {
     return p.lds && p.n_splits == 1 && !minmax && n_items >= 16 * kSeedItems;
@@ -1875,9 +1877,9 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
 #endif
         if (seeded_sweep(p, mm, n_items)) {
             rc = LGX_OK;
-            for (int64_t lo = 0, hi = kSeedItems; lo < n_items && rc == LGX_OK; lo = hi, hi *= 8) {
+            for (int64_t lo = 0, hi = kSeedItems; lo < n_items && rc == LGX_OK; lo = hi, hi *= 2) {
                 ScoreArgs st = a;
-                st.n_items = 2 * hi <= n_items ? hi : n_items;
+                st.n_items = 3 * hi < 2 * n_items ? hi : n_items;
                 st.seed_items = lo;
                 st.split_items = st.n_items - lo;
                 if (lo > 0) {

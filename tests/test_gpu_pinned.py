@@ -166,8 +166,8 @@ def test_full_sweep_masks_on_the_top_items(n_top, n_rand):
 
 
 def test_seeded_full_sweep_equals_one_sweep():
-    """Catalogs of >= 262 144 items run the full sweep in stages ([0, 16384), [16384, 131072), the
-    rest), each seeding the next.  Masks put every user's own best first-stage items (and random
+    """Catalogs of >= 262 144 items run the full sweep in stages ([0, 16384), [16384, 32768), ...
+    doubling, then the rest), each seeding the next.  Masks put every user's own best first-stage items (and random
     ones everywhere) out of play.  The lists must equal, as sets, the one-launch sweep
     (the min/max variant never seeds) and the float64 top-k of the unmasked items."""
     B, I, d, k = 256 * 256, 300_000, 256, 20

@@ -69,7 +69,47 @@ int main(int argc, char** argv) {
     std::printf("LGX_MASK_ABL=%d\n", LGX_MASK_ABL);
     if (timeit("full", launch<0, 0>, true)) return 1;
 #else
-    if (getenv("LAB_SEED")) {  // seeded sweep: exact top-k over items [0, S) first, then [S, I)
+    if (getenv("LAB_STAGES")) {  // seeded stages at the given item boundaries (comma list), vs one sweep
+        std::vector<int64_t> cut;
+        for (const char* c = getenv("LAB_STAGES"); *c;) {
+            cut.push_back(std::atoll(c));
+            while (*c && *c != ',') ++c;
+            if (*c) ++c;
+        }
+        cut.push_back(I);
+        uint64_t* susp = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + (size_t)B * p.n_splits * k * 8);
+        float* ps = reinterpret_cast<float*>(ws);
+        int32_t* pi = reinterpret_cast<int32_t*>(static_cast<char*>(ws) + (size_t)B * k * 4);
+        SplitPlan q = p;
+        q.n_splits = 1;
+        std::vector<ScoreArgs> st;
+        for (size_t j = 0; j < cut.size(); ++j) {
+            const int64_t lo = j ? cut[j - 1] : 0;
+            ScoreArgs x{Q, nullptr, items, B, cut[j], d, mp, mi, k, 1, cut[j] - lo, ps, pi, nullptr, susp,
+                        j ? ps : nullptr, j ? pi : nullptr, lo};
+            st.push_back(x);
+        }
+        ScoreArgs one{Q, nullptr, items, B, I, d, mp, mi, k, 1, I, ps, pi, nullptr, susp};
+        float best1 = 1e30f, bestS = 1e30f;
+        for (int r = 0; r < 3; ++r) {
+            HK(hipEventRecord(e0, nullptr));
+            if (launch<0, 0>(one, q, nullptr)) return 1;
+            HK(hipEventRecord(e1, nullptr));
+            HK(hipEventSynchronize(e1));
+            float ms;
+            HK(hipEventElapsedTime(&ms, e0, e1));
+            best1 = std::min(best1, ms);
+            HK(hipEventRecord(e0, nullptr));
+            for (auto& x : st)
+                if (launch<0, 0>(x, q, nullptr)) return 1;
+            HK(hipEventRecord(e1, nullptr));
+            HK(hipEventSynchronize(e1));
+            HK(hipEventElapsedTime(&ms, e0, e1));
+            bestS = std::min(bestS, ms);
+        }
+        std::printf("stages %s: one sweep %.2f ms, %zu stages %.2f ms (%.1f %%)\n", getenv("LAB_STAGES"), best1,
+                    st.size(), bestS, 100.0 * (best1 - bestS) / best1);
+    } else if (getenv("LAB_SEED")) {  // seeded sweep: exact top-k over items [0, S) first, then [S, I)
         const int64_t S = std::atoll(getenv("LAB_SEED"));
         const int masked = getenv("LAB_UNMASKED") ? 0 : 1;
         const int64_t* mp_ = masked ? mp : nullptr;
