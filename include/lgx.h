@@ -185,6 +185,8 @@ int lgx_score_topk_workspace(int64_t B, int64_t n_items, int k, size_t* ws_bytes
  *   Ranking: higher raw score first, ties -> lower item id.  out_val = raw score, or
  *   sigmoid(score) if apply_sigmoid.  minmax_out (NULL = skip) receives {min, max} of ALL raw
  *   scores (before masking) as f32[2].  k in [1, 256] (k <= 32 runs the LDS-staged bf16 kernel).
+ *   Full sweeps over >= 262144 items (and no minmax_out) run as several stream-ordered launches
+ *   over consecutive item ranges, each seeding the next through the workspace's lists.
  */
 int lgx_score_topk(const void* Q, const int64_t* user_rows, const void* items, int64_t B,
                    int64_t n_items, int64_t d, int dtype, const int64_t* mask_indptr,
