@@ -77,6 +77,7 @@ int main(int argc, char** argv) {
             if (*c) ++c;
         }
         cut.push_back(I);
+        const bool um = getenv("LAB_UNMASKED") != nullptr;
         uint64_t* susp = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + (size_t)B * p.n_splits * k * 8);
         float* ps = reinterpret_cast<float*>(ws);
         int32_t* pi = reinterpret_cast<int32_t*>(static_cast<char*>(ws) + (size_t)B * k * 4);
@@ -85,11 +86,11 @@ int main(int argc, char** argv) {
         std::vector<ScoreArgs> st;
         for (size_t j = 0; j < cut.size(); ++j) {
             const int64_t lo = j ? cut[j - 1] : 0;
-            ScoreArgs x{Q, nullptr, items, B, cut[j], d, mp, mi, k, 1, cut[j] - lo, ps, pi, nullptr, susp,
+            ScoreArgs x{Q, nullptr, items, B, cut[j], d, um ? nullptr : mp, um ? nullptr : mi, k, 1, cut[j] - lo, ps, pi, nullptr, susp,
                         j ? ps : nullptr, j ? pi : nullptr, lo};
             st.push_back(x);
         }
-        ScoreArgs one{Q, nullptr, items, B, I, d, mp, mi, k, 1, I, ps, pi, nullptr, susp};
+        ScoreArgs one{Q, nullptr, items, B, I, d, um ? nullptr : mp, um ? nullptr : mi, k, 1, I, ps, pi, nullptr, susp};
         float best1 = 1e30f, bestS = 1e30f;
         for (int r = 0; r < 3; ++r) {
             HK(hipEventRecord(e0, nullptr));
@@ -107,7 +108,7 @@ int main(int argc, char** argv) {
             HK(hipEventElapsedTime(&ms, e0, e1));
             bestS = std::min(bestS, ms);
         }
-        std::printf("stages %s: one sweep %.2f ms, %zu stages %.2f ms (%.1f %%)\n", getenv("LAB_STAGES"), best1,
+        std::printf("stages %s%s: one sweep %.2f ms, %zu stages %.2f ms (%.1f %%)\n", um ? "(unmasked) " : "", getenv("LAB_STAGES"), best1,
                     st.size(), bestS, 100.0 * (best1 - bestS) / best1);
     } else if (getenv("LAB_SEED")) {  // seeded sweep: exact top-k over items [0, S) first, then [S, I)
         const int64_t S = std::atoll(getenv("LAB_SEED"));
