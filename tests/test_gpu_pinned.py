@@ -202,6 +202,31 @@ def test_seeded_full_sweep_equals_one_sweep():
     assert (got >= kth - 1e-5 * kth.abs().clamp(min=1.0)).all()
 
 
+@pytest.mark.parametrize("d,k,rows", [(64, 1, False), (128, 7, True), (256, 32, False), (96, 20, True)])
+def test_seeded_sweep_shapes(d, k, rows):
+    """The seeded stages across the LDS kernel's shapes (d, k) and with user_rows: lists equal, as
+    sets, the one-launch sweep of the unseeded min/max variant."""
+    B, I = 256 * 256, 270_000
+    assert "seeded in stages" in ops.score_topk_plan(B, I, d, torch.bfloat16, k)
+    g = torch.Generator(device=DEV).manual_seed(31 + d + k)
+    n_q = B + 1000 if rows else B
+    Q = (torch.randn(n_q, d, device=DEV, generator=g) / 16).bfloat16()
+    items = (torch.randn(I, d, device=DEV, generator=g) / 16).bfloat16()
+    user_rows = torch.randperm(n_q, device=DEV, generator=g)[:B] if rows else None
+    m = torch.randint(0, I, (B, 30), device=DEV, generator=g).sort(1).values
+    keep = torch.ones_like(m, dtype=torch.bool)
+    keep[:, 1:] = m[:, 1:] != m[:, :-1]
+    indptr = torch.zeros(B + 1, dtype=torch.int64, device=DEV)
+    indptr[1:] = torch.cumsum(keep.sum(1), 0)
+    mask = (indptr, m[keep].to(torch.int32))
+    idx, val = lgx.score_topk(Q, items, k, user_rows=user_rows, mask=mask)
+    idx1, val1, _ = lgx.score_topk(Q, items, k, user_rows=user_rows, mask=mask, want_minmax=True)
+    ka, kb = torch.sort(idx.long(), 1), torch.sort(idx1.long(), 1)
+    assert torch.equal(ka.values, kb.values), "seeded lists differ from the one-launch sweep"
+    assert torch.equal(val.gather(1, ka.indices), val1.gather(1, kb.indices))
+    assert (idx >= 0).all()
+
+
 def test_c1_gowalla_shape_vs_oracle():
     cfg = CONFIGS["gowalla"]
     u, i = synth_edges(cfg, 2020, DEV)
