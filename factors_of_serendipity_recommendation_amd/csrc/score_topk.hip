@@ -23,6 +23,7 @@
 //     sorted partial list and a one-wave-per-user merge (register bitonic network) finishes, adds
 //     the masked tail when fewer than k unmasked items exist, applies the optional sigmoid.
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cfloat>
 #include <cstdlib>
@@ -1454,11 +1455,13 @@ __global__ __launch_bounds__(kDenseWaves * 64) void strat_label_lds(const void* 
     // T[j] = the score where label j starts (T[0] = -inf, T[n + 1] = +inf): the label of s is the
     // estimate e corrected by one compare on each side, s < T[e] and s >= T[e + 1]
     __shared__ float T[34];
+    __shared__ float2 TP[33];  // {T[j], T[j + 1]}: the estimate path's two thresholds in one 8-B read
     __shared__ uint32_t hc[kDenseUsers * kHistStride];  // hist != nullptr: per-user label counts
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, col = lane & 31;
-    if (threadIdx.x < 34)
-        T[threadIdx.x] = threadIdx.x == 0 ? -INFINITY : (threadIdx.x <= thr.n ? thr.t[threadIdx.x - 1] : INFINITY);
+    auto thr_at = [&](int j) { return j == 0 ? -INFINITY : (j <= thr.n ? thr.t[j - 1] : INFINITY); };
+    if (threadIdx.x < 34) T[threadIdx.x] = thr_at(threadIdx.x);
+    if (threadIdx.x < 33) TP[threadIdx.x] = make_float2(thr_at(threadIdx.x), thr_at(threadIdx.x + 1));
     if (hist)
         for (int e = threadIdx.x; e < kDenseUsers * kHistStride; e += kDenseWaves * 64) hc[e] = 0u;
     const int64_t L = blockIdx.x, kk = L >> 3;
@@ -1501,8 +1504,8 @@ __global__ __launch_bounds__(kDenseWaves * 64) void strat_label_lds(const void* 
         const float x = (sc - thr.base) * thr.inv;
         int l = (x >= (float)thr.n || x != x) ? thr.n : (x < 0.0f ? 0 : (int)x);  // NaN -> n, as label_of
         if (EST1) {  // the host proved |estimate - label| <= 1: one branch-free step each way
-            const int lo = l, up = l < thr.n ? l + 1 : l;
-            return (uint32_t)(l - (sc < T[lo] && l > 0 ? 1 : 0) + (sc >= T[up] && l < thr.n ? 1 : 0));
+            const float2 tp = TP[l];  // T[l], T[l + 1]
+            return (uint32_t)(l - (sc < tp.x && l > 0 ? 1 : 0) + (sc >= tp.y && l < thr.n ? 1 : 0));
         }
         while (l > 0 && sc < T[l]) --l;  // exact whatever the estimate
         while (l < thr.n && sc >= T[l + 1]) ++l;
@@ -1526,7 +1529,9 @@ __global__ __launch_bounds__(kDenseWaves * 64) void strat_label_lds(const void* 
                 const uint4 fr = *reinterpret_cast<const uint4*>(rowp + (((2 * c + h) ^ (col & 15)) * 16));
                 acc = F::mma(__builtin_bit_cast(typename F::chunk, fr), uf[c], acc);
             }
-            if (user_ok) {
+            // whole tiles (all but a split's last) skip the per-item bounds tests
+            auto emit = [&](auto whole_tag) {
+                constexpr bool WHOLE = decltype(whole_tag)::value;
                 uint32_t* hu = hc + (wave * kUsersPerWave + col) * kHistStride;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -1535,12 +1540,12 @@ __global__ __launch_bounds__(kDenseWaves * 64) void strat_label_lds(const void* 
                     const uint32_t l2 = label(acc[4 * q + 2]), l3 = label(acc[4 * q + 3]);
                     const uint32_t w = l0 | (l1 << 8) | (l2 << 16) | (l3 << 24);
                     if (hist) {  // items past the split's end are not counted
-                        if (it < i_end) atomicAdd(hu + l0, 1u);
-                        if (it + 1 < i_end) atomicAdd(hu + l1, 1u);
-                        if (it + 2 < i_end) atomicAdd(hu + l2, 1u);
-                        if (it + 3 < i_end) atomicAdd(hu + l3, 1u);
+                        if (WHOLE || it < i_end) atomicAdd(hu + l0, 1u);
+                        if (WHOLE || it + 1 < i_end) atomicAdd(hu + l1, 1u);
+                        if (WHOLE || it + 2 < i_end) atomicAdd(hu + l2, 1u);
+                        if (WHOLE || it + 3 < i_end) atomicAdd(hu + l3, 1u);
                     }
-                    if (VEC4 && it + 4 <= i_end) {
+                    if (VEC4 && (WHOLE || it + 4 <= i_end)) {
                         *reinterpret_cast<uint32_t*>(lab + it) = w;
                     } else {
 #pragma unroll
@@ -1548,6 +1553,10 @@ __global__ __launch_bounds__(kDenseWaves * 64) void strat_label_lds(const void* 
                             if (it + e < i_end) lab[it + e] = (int8_t)((w >> (8 * e)) & 255);
                     }
                 }
+            };
+            if (user_ok) {
+                if (i0 + 32 <= i_end) emit(std::true_type{});
+                else emit(std::false_type{});
             }
         }
         if (more) store_tile(buf ^ 1);
