@@ -4,6 +4,7 @@
 #   1. plain bench (the JSON line, with CPU baselines)
 #   2. --kernel-trace --stats under the bench (per-kernel durations)
 #   3. --pmc FETCH_SIZE and 4. --pmc WRITE_SIZE, separate passes (MI355X_MICROARCH.md HBM recipe)
+#   5. plain bench again, with the PMC bytes of this build in its line
 set -eo pipefail
 TAG=${1:?usage: tools/profile_round.sh <tag, e.g. r01>}
 ROOT=$(pwd)
@@ -27,4 +28,8 @@ timeout -k 10 900 rocprofv3 --pmc WRITE_SIZE --output-format csv --kernel-includ
 cd "$ROOT"
 python3 tools/pmc_summary.py "$TAG" --src "$OUT" --dst "$OUT/summary" > /dev/null
 rm -rf "$OUT/trace" "$OUT/fetch" "$OUT/write"   # raw rocprof output exceeds what gpurun copies back
+# 5. the plain bench again, now reading this build's PMC bytes (bench.py takes them from profiles/)
+cp "$OUT/summary/${TAG}_synth10m_pmc_traffic.json" "$ROOT/profiles/"
+echo "[profile] plain bench with this build's PMC traffic"
+timeout -k 10 900 python3 "$ROOT/bench.py" > "$OUT/bench_with_traffic.json" 2> "$OUT/bench_with_traffic.log"
 echo "[profile] done"
