@@ -150,3 +150,32 @@ def test_loader_parses_reference_format(tmp_path, mlls):
     u0 = int(mlls["test_users"][0])
     assert sorted(ds.testDict[u0]) == sorted(sx[sp_[0]:sp_[1]].tolist())
     assert np.array_equal(np.sort(ds.allPos[0]), np.sort(tx[tp[0]:tp[1]]))
+
+
+def test_bench_measured_traffic_per_call(tmp_path, monkeypatch):
+    """bench.measured_traffic: bytes of a committed PMC summary only for the library build that
+    made it; with calls_from, every dispatch of the kernels per library call (the seeded scoring
+    stages launch the sweep kernel several times per lgx_score_topk call)."""
+    import importlib.util
+    import json
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    (tmp_path / "profiles").mkdir()
+    doc = {"lib_sha256_16": "abc", "kernels": {"scoring": {
+        "score_topk_bf16_lds": {"hbm_bytes_per_launch": 100e9, "dispatches": 24},
+        "score_topk_finalize": {"hbm_bytes_per_launch": 1e9, "dispatches": 6}}}}
+    (tmp_path / "profiles" / "r09_cfg_pmc_traffic.json").write_text(json.dumps(doc))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "lib_sha", lambda: "abc")
+    ks = ["score_topk_bf16_lds", "score_topk_finalize"]
+    gb, src = bench.measured_traffic("cfg", "scoring", 1, ks, calls_from=("score_topk_finalize", 2))
+    assert src.endswith("r09_cfg_pmc_traffic.json")
+    assert abs(gb - (100 * 24 + 1 * 6) / 3) < 1e-9  # 3 calls: 6 finalize dispatches, 2 per call
+    gb1, _ = bench.measured_traffic("cfg", "scoring", 1, ks)
+    assert abs(gb1 - 101) < 1e-9                     # per-dispatch means, summed
+    monkeypatch.setattr(bench, "lib_sha", lambda: "other")
+    assert bench.measured_traffic("cfg", "scoring", 1, ks)[0] is None
+    assert bench.measured_traffic("cfg", "scoring", 2, ks)[0] is None
