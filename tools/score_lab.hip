@@ -16,7 +16,7 @@ int launch(const ScoreArgs& a, const SplitPlan& p, hipStream_t s) {
 
 int main(int argc, char** argv) {
     const int64_t B = argc > 1 ? std::atoll(argv[1]) : 131072;
-    const int64_t I = 1000000, d = 256, M = 50;
+    const int64_t I = getenv("LAB_I") ? std::atoll(getenv("LAB_I")) : 1000000, d = 256, M = 50;
     const int k = 20;
     void *Q, *items, *ws;
     int32_t* mi;
