@@ -69,7 +69,69 @@ int main(int argc, char** argv) {
     std::printf("LGX_MASK_ABL=%d\n", LGX_MASK_ABL);
     if (timeit("full", launch<0, 0>, true)) return 1;
 #else
-    if (getenv("LAB_STAGES")) {  // seeded stages at the given item boundaries (comma list), vs one sweep
+    if (getenv("LAB_TAILCONC")) {  // the bench plan: staged full sweep of B users + a split tail of T users,
+        // one stream after the other vs the tail on a second stream beside the stages
+        const int64_t T = std::atoll(getenv("LAB_TAILCONC"));
+        void *Qt, *wst;
+        HK(hipMalloc(&Qt, T * d * 2));
+        if (lgx_fill_normal(Qt, T * d, 1.0f / 16, 3, LGX_DTYPE_BF16, nullptr)) return 1;
+        const SplitPlan pt = plan_splits(T, I, LGX_DTYPE_BF16, d, k);
+        HK(hipMalloc(&wst, (size_t)T * pt.n_splits * k * 8 + 4096));
+        std::vector<int64_t> cut;
+        for (int64_t hi = 16384; 3 * hi < 2 * I; hi *= 2) cut.push_back(hi);
+        cut.push_back(I);
+        uint64_t* susp = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + (size_t)B * p.n_splits * k * 8);
+        float* ps = reinterpret_cast<float*>(ws);
+        int32_t* pi = reinterpret_cast<int32_t*>(static_cast<char*>(ws) + (size_t)B * k * 4);
+        SplitPlan q = p;
+        q.n_splits = 1;
+        std::vector<ScoreArgs> st;
+        for (size_t j = 0; j < cut.size(); ++j) {
+            const int64_t lo = j ? cut[j - 1] : 0;
+            ScoreArgs x{Q, nullptr, items, B, cut[j], d, mp, mi, k, 1, cut[j] - lo, ps, pi, nullptr, susp,
+                        j ? ps : nullptr, j ? pi : nullptr, lo};
+            st.push_back(x);
+        }
+        ScoreArgs tail{Qt, nullptr, items, T, I, d, nullptr, nullptr, k, pt.n_splits, pt.split_items,
+                       reinterpret_cast<float*>(wst),
+                       reinterpret_cast<int32_t*>(static_cast<char*>(wst) + (size_t)T * pt.n_splits * k * 4), nullptr,
+                       nullptr};
+        hipStream_t s2;
+        HK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+        hipEvent_t fork, join;
+        HK(hipEventCreate(&fork));
+        HK(hipEventCreate(&join));
+        float seq = 1e30f, conc = 1e30f, tl = 1e30f;
+        for (int r = 0; r < 3; ++r) {
+            float ms;
+            HK(hipEventRecord(e0, nullptr));
+            for (auto& x : st) if (launch<0, 0>(x, q, nullptr)) return 1;
+            if (launch<0, 0>(tail, pt, nullptr)) return 1;
+            HK(hipEventRecord(e1, nullptr));
+            HK(hipEventSynchronize(e1));
+            HK(hipEventElapsedTime(&ms, e0, e1));
+            seq = std::min(seq, ms);
+            HK(hipEventRecord(e0, nullptr));
+            if (launch<0, 0>(tail, pt, nullptr)) return 1;
+            HK(hipEventRecord(e1, nullptr));
+            HK(hipEventSynchronize(e1));
+            HK(hipEventElapsedTime(&ms, e0, e1));
+            tl = std::min(tl, ms);
+            HK(hipEventRecord(e0, nullptr));
+            HK(hipEventRecord(fork, nullptr));
+            HK(hipStreamWaitEvent(s2, fork, 0));
+            if (launch<0, 0>(tail, pt, s2)) return 1;
+            HK(hipEventRecord(join, s2));
+            for (auto& x : st) if (launch<0, 0>(x, q, nullptr)) return 1;
+            HK(hipStreamWaitEvent(nullptr, join, 0));
+            HK(hipEventRecord(e1, nullptr));
+            HK(hipEventSynchronize(e1));
+            HK(hipEventElapsedTime(&ms, e0, e1));
+            conc = std::min(conc, ms);
+        }
+        std::printf("B=%lld + tail %lld (splits %d): stages then tail %.2f ms (tail alone %.2f) | tail beside the stages %.2f ms (%.1f %%)\n",
+                    (long long)B, (long long)T, pt.n_splits, seq, tl, conc, 100.0 * (seq - conc) / seq);
+    } else if (getenv("LAB_STAGES")) {  // seeded stages at the given item boundaries (comma list), vs one sweep
         std::vector<int64_t> cut;
         for (const char* c = getenv("LAB_STAGES"); *c;) {
             cut.push_back(std::atoll(c));
