@@ -401,8 +401,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "rows.json"))
     ap.add_argument("--only", default="")
+    ap.add_argument("--lib", default=None, help="development: time another liblgx.so build")
     ap.add_argument("--reps", type=int, default=5)
     args = ap.parse_args()
+    if args.lib:
+        _lib.LIB_PATH = os.path.abspath(args.lib)
+        _lib._lib = None
     if not torch.cuda.is_available():
         raise SystemExit("bench_rows needs a GPU")
     torch.set_num_threads(CPU_THREADS)
