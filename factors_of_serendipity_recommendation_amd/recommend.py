@@ -218,6 +218,19 @@ def stratified_candidates(emb_user: torch.Tensor, emb_item: torch.Tensor, train:
     out_lists: List[List[int]] = []
     L = _lib.lib()
     st = ops._stream_ptr(dev)
+    pin = dev.type == "cuda"
+
+    def unpack(p):
+        # the host's list building for batch b runs while the GPU labels and selects batch b+1
+        ev, o_h, c_h = p
+        ev.synchronize()
+        o, c = o_h.numpy(), c_h.numpy()
+        rows = o.tolist()  # one C call for the whole batch; only short rows get trimmed
+        for j in np.flatnonzero(c < o.shape[1]).tolist():
+            rows[j] = rows[j][:c[j]]
+        out_lists.extend(rows)
+
+    pending = None
     for b0 in range(0, U, batch):
         b1 = min(U, b0 + batch)
         labels, hist = strat_labels(emb_user[b0:b1], emb_item, mp[b0:], mi, min16, inter16, num_fold, fused)
@@ -226,9 +239,26 @@ def stratified_candidates(emb_user: torch.Tensor, emb_item: torch.Tensor, train:
         _lib.check(L.lgx_strat_select(labels.data_ptr(), b1 - b0, I, hist.data_ptr(), num_fold + 1,
                                       tgt[b0:b1].contiguous().data_ptr(), (seed * 0x9E3779B97F4A7C15 + b0) % 2 ** 64,
                                       out.data_ptr(), K, cnt.data_ptr(), st), "lgx_strat_select")
-        o, c = out.cpu().numpy(), cnt.cpu().numpy()
-        out_lists.extend(o[j, :c[j]].tolist() for j in range(b1 - b0))
+        o_h = torch.empty(out.shape, dtype=torch.int32, pin_memory=pin)
+        c_h = torch.empty(cnt.shape, dtype=torch.int32, pin_memory=pin)
+        o_h.copy_(out, non_blocking=pin)
+        c_h.copy_(cnt, non_blocking=pin)
+        ev = torch.cuda.Event() if pin else None
+        if ev is not None:
+            ev.record()
+        if pending is not None:
+            unpack(pending)
+        pending = (ev if ev is not None else _Done(), o_h, c_h)
+    if pending is not None:
+        unpack(pending)
     return out_lists
+
+
+class _Done:
+    """Event stand-in for a batch whose copies already completed (synchronous, non-CUDA device)."""
+
+    def synchronize(self) -> None:
+        pass
 
 
 def create_candidates_stratification(dataset_name: str, seed: int, K_c: int = 1000, num_fold: int = 10,

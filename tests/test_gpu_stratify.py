@@ -172,3 +172,25 @@ def test_fused_stratified_candidates_equal_two_step():
     a = recommend.stratified_candidates(Eu, Ei, train, targets, seed=3, batch=256, fused=True)
     b = recommend.stratified_candidates(Eu, Ei, train, targets, seed=3, batch=256, fused=False)
     assert a == b
+
+
+def test_stratified_candidates_pipelined_batches_equal_per_batch_select():
+    """stratified_candidates overlaps the host unpacking of batch b with batch b+1 on the GPU: the
+    lists equal a synchronous per-batch labels + select with the same per-batch seeds, in order,
+    over 3 batches (the last partial) and varied per-user targets."""
+    eu, ei, train = _setup(seed=9, U=600, I=4000, d=64)
+    Eu, Ei = torch.from_numpy(eu).to(DEV), torch.from_numpy(ei).to(DEV)
+    rng = np.random.default_rng(2)
+    targets = rng.integers(50, 400, len(train)).tolist()
+    got = recommend.stratified_candidates(Eu, Ei, train, targets, seed=7, batch=256)
+    min16, inter16 = recommend.stratification_bounds(Eu, Ei, 10, 0.1)
+    mp, mi = ops.lists_to_device_csr(train, DEV, sort=True)
+    K = max(targets)
+    want = []
+    for b0 in range(0, len(train), 256):
+        b1 = min(len(train), b0 + 256)
+        lab, hist = recommend.strat_labels(Eu[b0:b1], Ei, mp[b0:], mi, min16, inter16, 10, None)
+        o, c = _select(lab, hist, targets[b0:b1], seed=(7 * 0x9E3779B97F4A7C15 + b0) % 2 ** 64, stride=K)
+        want.extend(o[j, :c[j]].tolist() for j in range(b1 - b0))
+    assert len(got) == len(train)
+    assert got == want
