@@ -7,10 +7,12 @@ Workload (BASELINE.json): the propagation metric is quoted at 1/2/4/8 GPUs on co
 ("Synthetic 10M users x 1M items, 500M edges, K=3, d=128, row-sharded with RCCL all-gather"),
 which fits one MI355X (CSR 8 GB + tables < 30 GB of 288 GB), so it is the N=1 workload too and the
 total graph is fixed as N grows (strong scaling).  One step = one full K-layer propagation
-(LightGCN.computer(), model.py:145-177).  `value` is the bf16-storage / fp32-accumulate run (SURVEY
-C4: "fp32 parity; bf16 perf"); the same line carries the fp32-storage run (the north-star
-precision) under "fp32".  The scoring metric (configs[4]: user x item MFMA scoring + train mask +
-top-20, d=256 bf16, 1M items) is reported under "scoring": one step scores a fixed batch of query
+(LightGCN.computer(), model.py:145-177).  `value` / `dtype` are the fp32-storage run, the
+reference's precision (model.py:163-176); the same line carries the bf16-storage / fp32-accumulate
+run ("fp32 parity; bf16 perf") under "bf16".  The scoring metric (configs[4]: user x
+item MFMA scoring + train mask + top-20, d=256, 1M items) is reported under "scoring" in fp32 (the
+reference's precision, model.py:183; a 262,144-user batch so the f32-MFMA leg fits the run) and
+under "scoring_bf16" (SURVEY C5's bf16 inputs, 1M users): one step scores a fixed batch of query
 users against the full catalog, the batch split across ranks.
 
 value = K * nnz(A^) * steps / t  (edges/s), t = max over ranks of the barrier-bracketed loop.
@@ -52,6 +54,7 @@ from factors_of_serendipity_recommendation_amd.synth import CONFIGS, synth_edges
 
 HBM_PEAK = 8.0e12        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BF16_MFMA_PEAK = 2.5e15  # dense bf16 MFMA spec
+F32_MFMA_PEAK = 157.3e12  # f32-input MFMA (v_mfma_f32_32x32x2_f32), MI355X_MICROARCH.md:42
 L2_BYTES = 4 << 20       # per XCD
 METRIC = "LightGCN prop edges/s + full-catalog score items/s at 1/2/4/8 MI355X"
 CALIB = "profiles/r02_fetch_calibration.json"
@@ -134,13 +137,27 @@ def cold_gather_rows(A, d: int, s: int) -> tuple:
     return total - hot, R, hot / max(1, total)
 
 
-def layer_models(A, d: int, s: int, mode: int, n_prev: int = 0) -> dict:
+def cold_gather_cols(Aop, d: int, s: int) -> tuple:
+    """cold_gather_rows for a rectangular shard operator (N>1): it gathers ONE table (its columns),
+    whose L2 hot set is the top-R columns by in-operator count (bincount of the column ids)."""
+    cnt = torch.bincount(Aop.indices.to(torch.int64), minlength=Aop.n_cols)
+    R = max(1, L2_BYTES // (d * s))
+    total = int(cnt.sum())
+    hot = int(torch.topk(cnt, min(R, cnt.numel())).values.sum()) if cnt.numel() else 0
+    return total - hot, R, hot / max(1, total)
+
+
+def layer_models(A, d: int, s: int, mode: int, n_prev: int = 0, shard_op: bool = False) -> dict:
+    """Byte models of one layer launch of operator A (the same conventions at N=1 and N>1): CSR
+    stream + epilogue + gathers of rows outside the per-XCD L2 hot set of each gathered table."""
     nnz, rows, N = A.nnz, A.n_rows, A.n_cols
     csr = nnz * 8 + 8 * (rows + 1)
     epi = epilogue_bytes(mode, rows, d, s, n_prev)
-    cold, R, hot_frac = cold_gather_rows(A, d, s)
+    cold, R, hot_frac = cold_gather_cols(A, d, s) if shard_op else cold_gather_rows(A, d, s)
+    floor = nnz * 8 + (rows + N) * d * s if shard_op else nnz * 8 + 2 * N * d * s
     return {"model": csr + epi + cold * d * s, "gathered": csr + epi + nnz * d * s,
-            "floor": nnz * 8 + 2 * N * d * s, "hot_rows": R, "hot_frac": hot_frac}
+            "floor": floor, "hot_rows": R, "hot_frac": hot_frac,
+            "kernel": ops.spmm_kernel_name(d, torch.bfloat16 if s == 2 else torch.float32, A.plan.seg_len)}
 
 
 def calibration() -> dict:
@@ -189,6 +206,8 @@ def make_step(A, E0, K, d, dtype, world, cfg, rank, timings):
     prop = ShardedPropagation(shard, E0[:cfg.n_users], E0[cfg.n_users:], K)
     models = {}
 
+    # the N=1 conventions per shard operator: cache-aware model (hot set of the table it gathers),
+    # kernel named from the operator's own launch plan
     def layer_fn(Aop, X, mode, **kw):
         if step.record:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -196,13 +215,9 @@ def make_step(A, E0, K, d, dtype, world, cfg, rank, timings):
         ops.propagate_layer(Aop, X, mode, **kw)
         if step.record:
             e1.record()
-            nnz, rows = Aop.nnz, Aop.n_rows
             key = (id(Aop), mode)
             if key not in models:
-                epi = epilogue_bytes(mode, rows, d, es)
-                csr = nnz * 8 + 8 * (rows + 1)
-                models[key] = {"model": csr + epi + nnz * d * es, "gathered": csr + epi + nnz * d * es,
-                               "floor": nnz * 8 + rows * d * es + Aop.n_cols * d * es, "hot_rows": 0, "hot_frac": 0.0}
+                models[key] = layer_models(Aop, d, es, mode, shard_op=True)
             timings.append((e0, e1, models[key]))
 
     def stack_fn(Aop, X, E0r, prev, out, n_mean):
@@ -212,13 +227,9 @@ def make_step(A, E0, K, d, dtype, world, cfg, rank, timings):
         ops.propagate_layer_stack(Aop, X, E0r, prev, out, n_mean)
         if step.record:
             e1.record()
-            nnz, rows = Aop.nnz, Aop.n_rows
             key = (id(Aop), _lib.LGX_LAYER_STACK)
             if key not in models:
-                epi = epilogue_bytes(_lib.LGX_LAYER_STACK, rows, d, es, len(prev))
-                csr = nnz * 8 + 8 * (rows + 1)
-                models[key] = {"model": csr + epi + nnz * d * es, "gathered": csr + epi + nnz * d * es,
-                               "floor": nnz * 8 + rows * d * es + Aop.n_cols * d * es, "hot_rows": 0, "hot_frac": 0.0}
+                models[key] = layer_models(Aop, d, es, _lib.LGX_LAYER_STACK, len(prev), shard_op=True)
             timings.append((e0, e1, models[key]))
 
     prop.layer_fn = layer_fn
@@ -255,17 +266,18 @@ def bench_propagation(args, rank, world, A, cfg, dtype, steps, warmup):
     launch_s = np.array([e0.elapsed_time(e1) for e0, e1, _ in timings]) / 1e3
     mean_launch_s = float(launch_s.mean())
     mean = {key: float(np.mean([m[key] for _, _, m in timings])) for key in ("model", "gathered", "floor")}
-    hot_rows, hot_frac = timings[0][2]["hot_rows"], timings[0][2]["hot_frac"]
+    hot_rows = timings[0][2]["hot_rows"]
+    hot_frac = float(np.mean([m["hot_frac"] for _, _, m in timings]))
+    kernels = sorted({m["kernel"] for _, _, m in timings})
     traffic, tsrc = measured_traffic(cfg.name, dname, world, ["spmm_segments", "spmm_fixup"])
     achieved = mean["model"] / mean_launch_s
     roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": achieved / HBM_PEAK, "traffic": traffic,
-            "kernel": "spmm_segments (+spmm_fixup): " + ops.spmm_kernel_name(d, dtype, A.plan.seg_len if world == 1
-                                                                             else 8192),
+            "kernel": "spmm_segments (+spmm_fixup): " + ", ".join(kernels),
             "mean_launch_ms": mean_launch_s * 1e3,
             "bytes_model": "cache-aware: CSR + epilogue + gathers of rows outside the per-XCD L2 hot set "
-                           f"(top {hot_rows} rows per table by degree = {hot_frac:.3f} of gathers)"
-                           if world == 1 else "per-rank operators, every gather counted",
+                           f"(top {hot_rows} rows per gathered table = {hot_frac:.3f} of gathers)"
+                           + ("" if world == 1 else "; per-rank pull / push operators, each its own hot set"),
             "bytes_per_launch": int(mean["model"]),
             "floor_bytes_per_launch": int(mean["floor"]), "floor_rate_gbs": mean["floor"] / mean_launch_s / 1e9,
             "floor_frac": mean["floor"] / mean_launch_s / HBM_PEAK,
@@ -333,13 +345,16 @@ def cpu_baseline(A, E0, cfg, target_nnz):
                       f"[{A.n_cols},{cfg.d}] table, {secs:.1f}s; per-edge rate extrapolated to the whole graph"}
 
 
-def bench_scoring(args, rank, world):
-    """configs[4]: d=256 bf16, 1M items, top-20 with a train mask; users split over ranks."""
+def bench_scoring(args, rank, world, dtype, B_total, steps, with_cpu):
+    """configs[4]: d=256, 1M items, top-20 with a 50-item train mask; users split over ranks.
+    dtype float32 = the reference's precision (model.py:183 fp32 matmul; score_topk_kernel<f32>,
+    v_mfma_f32_32x32x2_f32, against the 157.3 TF f32 MFMA peak); bfloat16 = SURVEY C5's inputs
+    (score_topk_bf16_lds, against 2.5 PF)."""
     d, n_items, k = 256, args.score_items, 20
-    B_total = args.score_users
     B = B_total // world
-    items = lgx.fill_normal((n_items, d), 1.0 / 16, 4242, dtype=torch.bfloat16)
-    Q = lgx.fill_normal((B, d), 1.0 / 16, 777 + rank, dtype=torch.bfloat16)
+    f32 = dtype == torch.float32
+    items = lgx.fill_normal((n_items, d), 1.0 / 16, 4242, dtype=dtype)
+    Q = lgx.fill_normal((B, d), 1.0 / 16, 777 + rank, dtype=dtype)
     g = torch.Generator(device="cuda")
     g.manual_seed(99 + rank)
     per = 50
@@ -350,7 +365,7 @@ def bench_scoring(args, rank, world):
     barrier_sync(world)
     ev = []
     t_start = time.perf_counter()
-    steps = max(1, args.score_steps)
+    steps = max(1, steps)
     for _ in range(steps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -361,21 +376,25 @@ def bench_scoring(args, rank, world):
     elapsed = max_over_ranks(time.perf_counter() - t_start, world)
     mean_launch = float(np.mean([a.elapsed_time(b) for a, b in ev])) / 1e3
     flops = 2.0 * B * n_items * d
-    plan = ops.score_topk_plan(B, n_items, d, torch.bfloat16, k)
+    plan = ops.score_topk_plan(B, n_items, d, dtype, k)
+    peak = F32_MFMA_PEAK if f32 else BF16_MFMA_PEAK
+    sweep = "score_topk_kernel" if f32 else "score_topk_bf16_lds"
     # per lgx_score_topk call: every stage of every user range (finalize runs once per range)
-    traffic, tsrc = measured_traffic(args.config, "scoring", world, ["score_topk_bf16_lds", "score_topk_finalize"],
+    traffic, tsrc = measured_traffic(args.config, "scoring_f32" if f32 else "scoring", world,
+                                     [sweep, "score_topk_finalize"],
                                      calls_from=("score_topk_finalize", plan.count("; ") + 1))
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if with_cpu and rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = scoring_cpu_baseline(Q, items, pos, k, args.cpu_score_users)
-    return {"value": B_total * n_items * steps / elapsed, "unit": "items/s", "users_per_step": B_total,
-            "n_items": n_items, "d": d, "k": k, "dtype": "bf16", "ms_per_step": elapsed / steps * 1e3,
-            "plan": plan,
-            "roofline": {"bound": "mfma", "achieved": flops / mean_launch / 1e12, "peak": BF16_MFMA_PEAK / 1e12,
-                         "unit": "TFLOP/s", "frac": flops / mean_launch / BF16_MFMA_PEAK, "traffic": traffic,
+    return {"value": B * world * n_items * steps / elapsed, "unit": "items/s", "users_per_step": B * world,
+            "n_items": n_items, "d": d, "k": k, "dtype": "f32" if f32 else "bf16",
+            "ms_per_step": elapsed / steps * 1e3, "steps": steps, "plan": plan,
+            "roofline": {"bound": "mfma", "achieved": flops / mean_launch / 1e12, "peak": peak / 1e12,
+                         "unit": "TFLOP/s", "frac": flops / mean_launch / peak, "traffic": traffic,
                          "traffic_unit": "GB/call", "traffic_source": tsrc,
-                         "kernel": "score_topk_bf16_lds (+ score_topk_finalize, both inside the timed launch)",
-                         "launch": "one lgx_score_topk call: its seeded stages and split tail"},
+                         "kernel": f"{sweep} (+ score_topk_finalize, both inside the timed launch)",
+                         "launch": "one lgx_score_topk call: " + ("its seeded stages and split tail" if not f32
+                                                                  else "its catalog-split launches")},
             "cpu_baseline": cpu}
 
 
@@ -402,17 +421,19 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="synth10m", choices=sorted(CONFIGS))
-    ap.add_argument("--dtype", default=None, choices=[None, "bf16", "f32"])
-    ap.add_argument("--score-users", type=int, default=1_000_000)
+    ap.add_argument("--dtype", default="f32", choices=["bf16", "f32"],
+                    help="storage dtype of the headline propagation run (f32 = the reference's, model.py:163-176)")
+    ap.add_argument("--score-users", type=int, default=1_000_000, help="bf16 scoring leg users (configs[4])")
+    ap.add_argument("--score-f32-users", type=int, default=262_144, help="fp32 scoring leg users")
     ap.add_argument("--score-items", type=int, default=1_000_000)
     ap.add_argument("--score-steps", type=int, default=2)
     ap.add_argument("--cpu-nnz", type=int, default=40_000_000)
     ap.add_argument("--cpu-score-users", type=int, default=4000)
-    ap.add_argument("--fp32-steps", type=int, default=5, help="timed steps of the fp32-storage run")
-    ap.add_argument("--no-fp32", action="store_true")
+    ap.add_argument("--extra-steps", type=int, default=10, help="timed steps of the other-dtype propagation run")
+    ap.add_argument("--no-extra-dtype", action="store_true", help="skip the other-dtype propagation run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scoring", action="store_true")
-    ap.add_argument("--no-propagation", action="store_true", help="development: scoring leg only")
+    ap.add_argument("--no-propagation", action="store_true", help="development: scoring legs only")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -432,13 +453,23 @@ def main():
     if world != args.gpus:
         log(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}")
 
+    def scoring_legs():
+        if args.no_scoring:
+            return None, None
+        f32 = bench_scoring(args, rank, world, torch.float32, args.score_f32_users, args.score_steps, True)
+        torch.cuda.empty_cache()
+        bf16 = bench_scoring(args, rank, world, torch.bfloat16, args.score_users, args.score_steps, False)
+        bf16["cpu_baseline"] = "see scoring.cpu_baseline (the reference's fp32 procedure)"
+        torch.cuda.empty_cache()
+        return f32, bf16
+
     if args.no_propagation:
-        sc = bench_scoring(args, rank, world)
+        sc, sc16 = scoring_legs()
         if rank == 0:
-            print(json.dumps({"metric": METRIC, "scoring": sc}), flush=True)
+            print(json.dumps({"metric": METRIC, "scoring": sc, "scoring_bf16": sc16}), flush=True)
         return
     cfg = CONFIGS[args.config]
-    main_dtype = torch.bfloat16 if (args.dtype or cfg.dtype) == "bf16" else torch.float32
+    main_dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     t0 = time.time()
     if world == 1:
         A = synth_graph(cfg, seed=2020, device="cuda")
@@ -457,15 +488,18 @@ def main():
         cpu = cpu_baseline(A, res["E0"], cfg, args.cpu_nnz)
     res.pop("E0", None)
     torch.cuda.empty_cache()
-    fp32 = None
-    if main_dtype == torch.bfloat16 and not args.no_fp32:
-        fp32 = bench_propagation(args, rank, world, A, cfg, torch.float32, max(1, args.fp32_steps),
-                                 max(1, min(2, args.warmup)))
-        fp32.pop("E0", None)
-        fp32["note"] = "fp32 embedding storage (the north-star precision), same graph and kernel family"
+    extra = None
+    if not args.no_extra_dtype:
+        other = torch.float32 if main_dtype == torch.bfloat16 else torch.bfloat16
+        extra = bench_propagation(args, rank, world, A, cfg, other, max(1, args.extra_steps),
+                                  max(1, min(2, args.warmup)))
+        extra.pop("E0", None)
+        extra["note"] = ("bf16 embedding storage / fp32 accumulation (SURVEY C4's perf mode), same graph and "
+                         "kernel family" if other == torch.bfloat16 else
+                         "fp32 embedding storage (the reference's precision), same graph and kernel family")
     del A
     torch.cuda.empty_cache()
-    scoring = None if args.no_scoring else bench_scoring(args, rank, world)
+    scoring, scoring16 = scoring_legs()
     line = {
         "metric": METRIC, "value": res["value"], "unit": "edges/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": res["ms_per_step"], "higher_is_better": True, "scaling": "strong",
@@ -475,7 +509,9 @@ def main():
                    "parallelism": f"row-shard{world}" if world > 1 else "single"},
         "process_group": ({"world_size": dist.get_world_size(), "backend": dist.get_backend()} if world > 1
                           else None),
-        "roofline": res["roofline"], "cpu_baseline": cpu, "fp32": fp32, "scoring": scoring,
+        "roofline": res["roofline"], "cpu_baseline": cpu,
+        ("bf16" if extra and extra["dtype"] == "bf16" else "fp32"): extra,
+        "scoring": scoring, "scoring_bf16": scoring16,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)

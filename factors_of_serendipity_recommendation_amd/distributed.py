@@ -121,8 +121,13 @@ def make_shard_from_edges(users: torch.Tensor, items: torch.Tensor, n_users: int
     the one make_shard cuts from the full operator.  Saves every rank the 1e9-nnz CSR build at C4."""
     dev = users.device
     u64 = users.to(torch.int64)
-    if u64.numel() > 1 and bool((u64[1:] < u64[:-1]).any()):
-        raise ValueError("make_shard_from_edges: edges must be sorted by user")
+    if u64.numel() > 1:
+        # sorted by (user, item) AND unique: a repeated edge would double-count both degrees and
+        # keep both entries, unsorted items would break the CSR order -- either way not make_shard's
+        # operator.  One vectorised comparison of the packed keys.
+        key = u64 * n_items + items.to(torch.int64)
+        if bool((key[1:] <= key[:-1]).any()):
+            raise ValueError("make_shard_from_edges: edges must be unique and sorted by (user, item)")
     deg_u = torch.bincount(u64, minlength=n_users).cpu().numpy()
     deg_i = torch.bincount(items.to(torch.int64), minlength=n_items).cpu().numpy()
     ip = np.zeros(n_users + 1, dtype=np.int64)
@@ -180,11 +185,15 @@ class ShardedPropagation:
 
     def __init__(self, shard: Shard, E0_user: torch.Tensor, E0_item: torch.Tensor, K: int,
                  group=None, layer_fn: Optional[LayerFn] = None, epilogue_fn: Optional[LayerFn] = None,
-                 stack_fn: Optional[LayerFn] = None):
+                 stack_fn: Optional[LayerFn] = None, force_collectives: bool = False):
         """E0_user / E0_item: the FULL layer-0 tables in global row order (replicated input, as every
         rank holds the embedding parameters); dtype f32 or bf16.  The user side keeps its K-1 layer
         tables and forms the mean in the last pull (stack_fn = lgx_propagate_layer_stack), as the
-        single-GPU lgx_propagate does; the item side keeps the f32 running sum of its own block."""
+        single-GPU lgx_propagate does; the item side keeps the f32 running sum of its own block.
+
+        force_collectives: issue the reduce-scatter / all-gather even at world 1 (where they are
+        copies), so that a one-GPU RCCL group runs the async collective stream ordering the
+        overlap depends on."""
         self.s = shard
         self.K = K
         self.group = group
@@ -209,8 +218,9 @@ class ShardedPropagation:
         self.acc_i = torch.zeros((s.n_i_local, d), dtype=torch.float32, device=dev)
         self.out_u = torch.zeros((s.n_u_local, d), dtype=torch.float32, device=dev)
         self.out_i = torch.zeros((s.n_i_local, d), dtype=torch.float32, device=dev)
+        self._collective = s.world > 1 or force_collectives
         # gloo cannot reduce-scatter device tensors: all-reduce + slice there (tests only)
-        self._rs_native = s.world == 1 or not (dev.type == "cuda" and dist.get_backend(group) == "gloo")
+        self._rs_native = self._collective and not (dev.type == "cuda" and dist.get_backend(group) == "gloo")
 
     @staticmethod
     def _buf(k: int) -> int:
@@ -227,7 +237,7 @@ class ShardedPropagation:
 
     def _reduce_scatter(self):
         """yi = this rank's block of sum over ranks of P."""
-        if self.s.world == 1:
+        if not self._collective:
             self.yi.copy_(self.P)
             return None
         if self._rs_native:
@@ -238,7 +248,7 @@ class ShardedPropagation:
         return None
 
     def _all_gather(self, table: torch.Tensor):
-        if self.s.world == 1:
+        if not self._collective:
             table.copy_(self.send_i)
             return None
         return dist.all_gather_into_tensor(table, self.send_i, group=self.group, async_op=True)
@@ -289,7 +299,7 @@ class ShardedPropagation:
             slab = torch.zeros((pad, self.d), dtype=torch.float32, device=loc.device)
             slab[:loc.shape[0]] = loc
             full = torch.empty((s.world * pad, self.d), dtype=torch.float32, device=loc.device)
-            if s.world > 1:
+            if self._collective:
                 dist.all_gather_into_tensor(full, slab, group=self.group)
             else:
                 full.copy_(slab)

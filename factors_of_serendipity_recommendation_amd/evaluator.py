@@ -10,6 +10,7 @@ References:
 """
 from __future__ import annotations
 
+import itertools
 from typing import Dict, List, Sequence
 
 import numpy as np
@@ -34,26 +35,35 @@ def eval_score_matrix_foldout(score_matrix, test_items, top_k: int = 20, thread_
 
 # --------------------------------------------------------------------------- PyTorch Test metrics
 def _label(test_data: Sequence[Sequence[int]], pred: np.ndarray) -> np.ndarray:
-    """utils.getLabel (code/utils.py:277-285)."""
-    r = []
-    for i in range(len(test_data)):
-        gt = set(int(x) for x in test_data[i])
-        r.append(np.array([int(x) in gt for x in pred[i]], dtype=float))
-    return np.array(r).astype("float")
+    """utils.getLabel (code/utils.py:277-285): r[i, j] = 1.0 if pred[i, j] is in test_data[i].
+    One sorted-key membership search for the whole batch instead of a set per user."""
+    pred = np.asarray(pred, dtype=np.int64)
+    n = len(test_data)
+    if pred.ndim != 2 or pred.shape[0] != n:
+        raise ValueError(f"pred must be [{n}, k]")
+    lens = np.fromiter(map(len, test_data), dtype=np.int64, count=n)
+    flat = np.fromiter(itertools.chain.from_iterable(test_data), dtype=np.int64, count=int(lens.sum()))
+    if flat.size == 0 or pred.size == 0:
+        return np.zeros(pred.shape, dtype=float)
+    M = int(max(flat.max(), pred.max())) + 1
+    keys = np.unique(np.repeat(np.arange(n, dtype=np.int64), lens) * M + flat)
+    q = np.arange(n, dtype=np.int64)[:, None] * M + pred
+    pos = np.minimum(np.searchsorted(keys, q), keys.size - 1)
+    return ((keys[pos] == q) & (pred >= 0)).astype(float)
 
 
 def test_one_batch(rating_k: np.ndarray, ground_true: Sequence[Sequence[int]], topks: Sequence[int]) -> Dict:
-    """Procedure.test_one_batch (Procedure.py:60-72) with RecallPrecision_ATk / NDCGatK_r."""
+    """Procedure.test_one_batch (Procedure.py:60-72) with RecallPrecision_ATk / NDCGatK_r
+    (code/utils.py:218-262), vectorised over users: the same float64 arrays as the reference's
+    per-user loops, reduced in the same order, so the sums are identical."""
     r = _label(ground_true, rating_k)
     pre, rec, ndcg = [], [], []
-    recall_n = np.array([len(ground_true[i]) for i in range(len(ground_true))])
+    recall_n = np.fromiter(map(len, ground_true), dtype=np.int64, count=len(ground_true))
     for k in topks:
         right = r[:, :k].sum(1)
         rec.append(np.sum(right / recall_n))
         pre.append(np.sum(right) / k)
-        tm = np.zeros((len(r), k))
-        for i, items in enumerate(ground_true):
-            tm[i, :min(k, len(items))] = 1
+        tm = (np.arange(k)[None, :] < np.minimum(k, recall_n)[:, None]).astype(float)
         idcg = np.sum(tm * 1. / np.log2(np.arange(2, k + 2)), axis=1)
         dcg = np.sum(r[:, :k] * (1. / np.log2(np.arange(2, k + 2))), axis=1)
         idcg[idcg == 0.] = 1.
@@ -91,7 +101,8 @@ def batch_test(user_emb: torch.Tensor, item_emb: torch.Tensor, users_to_test: Se
                train_items: Dict[int, Sequence[int]], test_set: Dict[int, Sequence[int]],
                Ks: Sequence[int] = (20,), train_set_flag: int = 0) -> Dict:
     """batch_test.test (batch_test.py:25-84): raw dot-product ratings, training items set to -inf
-    (train_set_flag=0), top-max(Ks), fold-out curves, mean over users."""
+    and the test set as truth (train_set_flag=0, :57-65), or no mask and the train items as truth
+    (train_set_flag=1, :66-68); top-max(Ks), fold-out curves, float32 mean over users."""
     top_show = np.sort(np.asarray(Ks))
     max_top = int(max(top_show))
     dev = user_emb.device
@@ -99,7 +110,7 @@ def batch_test(user_emb: torch.Tensor, item_emb: torch.Tensor, users_to_test: Se
     rows = torch.as_tensor(users, dtype=torch.int64, device=dev)
     if train_set_flag == 0:
         truths = [test_set[u] for u in users]
-        mask = ops.lists_to_device_csr([train_items.get(u, []) for u in users], dev, sort=True)
+        mask = ops.lists_to_device_csr([train_items[u] for u in users], dev, sort=True)  # KeyError as :64
     else:
         truths = [train_items[u] for u in users]
         mask = None

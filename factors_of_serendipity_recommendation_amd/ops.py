@@ -108,12 +108,20 @@ def propagate(A: CSRGraph, E0: torch.Tensor, K: int, out: Optional[torch.Tensor]
 
 
 # ------------------------------------------------------------------------------------ scoring
+def check_pair(Q: torch.Tensor, items: torch.Tensor) -> None:
+    """Query rows and item rows of one scoring launch: same dtype and the same d (the kernels read
+    both with one row stride)."""
+    if Q.dtype != items.dtype:
+        raise TypeError("Q and items must share a dtype")
+    if Q.dim() != 2 or items.dim() != 2 or Q.shape[1] != items.shape[1]:
+        raise ValueError(f"Q {tuple(Q.shape)} and items {tuple(items.shape)} must be [*, d] with one d")
+
+
 def score_dense(Q: torch.Tensor, items: torch.Tensor, user_rows: Optional[torch.Tensor] = None,
                 apply_sigmoid: bool = False) -> torch.Tensor:
     """[B, I] scores (getUsersRating, model.py:179-184 / TF batch_ratings, LightGCN.py:148)."""
     require_gpu(Q, items, user_rows)
-    if Q.dtype != items.dtype:
-        raise TypeError("Q and items must share a dtype")
+    check_pair(Q, items)
     Q = Q.contiguous()
     items = items.contiguous()
     B = user_rows.numel() if user_rows is not None else Q.shape[0]
@@ -128,21 +136,28 @@ def score_dense(Q: torch.Tensor, items: torch.Tensor, user_rows: Optional[torch.
 def lists_to_device_csr(lists: Sequence[Sequence[int]], device, sort: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
     """Ragged python lists -> (indptr int64 [n+1], indices int32) on the device.  A
     ``dataloader.PosLists`` (already sorted and de-duplicated) is packed on the device directly."""
+    import itertools
     import numpy as np
     if hasattr(lists, "device_csr"):
         ip, ix = lists.device_csr(device)
         return ip, ix.to(torch.int32)
-    lens = np.fromiter((len(l) for l in lists), dtype=np.int64, count=len(lists))
+    lens = np.fromiter(map(len, lists), dtype=np.int64, count=len(lists))
     indptr = np.zeros(len(lists) + 1, dtype=np.int64)
     np.cumsum(lens, out=indptr[1:])
-    if indptr[-1]:
-        parts = [np.asarray(l, dtype=np.int32) for l in lists]
-        if sort:
-            parts = [np.sort(p) for p in parts]
-        flat = np.concatenate(parts).astype(np.int32)
-    else:
-        flat = np.zeros(1, dtype=np.int32)
-    return torch.from_numpy(indptr).to(device), torch.from_numpy(flat).to(device)
+    total = int(indptr[-1])
+    if not total:
+        return torch.from_numpy(indptr).to(device), torch.zeros(1, dtype=torch.int32, device=device)
+    # one flat pass over the Python ints (no per-list array), the per-row sort as one sort of
+    # (row << 32 | item) keys on the device
+    flat = np.fromiter(itertools.chain.from_iterable(lists), dtype=np.int64, count=total)
+    if not sort:
+        return torch.from_numpy(indptr).to(device), torch.from_numpy(flat.astype(np.int32)).to(device)
+    if flat.min() < 0 or flat.max() >= 2 ** 31:
+        raise ValueError("list entries must be in [0, 2^31)")
+    rows = np.repeat(np.arange(len(lists), dtype=np.int64), lens)
+    key = torch.from_numpy((rows << 32) | flat).to(device)
+    key = torch.sort(key).values
+    return torch.from_numpy(indptr).to(device), (key & 0xFFFFFFFF).to(torch.int32)
 
 
 def parse_lines(text: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
@@ -206,8 +221,7 @@ def score_topk(Q: torch.Tensor, items: torch.Tensor, k: int, user_rows: Optional
     mask = (indptr int64 [B+1], indices int32) with each row's excluded items SORTED ascending.
     Returns (idx int32 [B,k], val f32 [B,k]) or (idx, val, minmax f32[2])."""
     require_gpu(Q, items, user_rows)
-    if Q.dtype != items.dtype:
-        raise TypeError("Q and items must share a dtype")
+    check_pair(Q, items)
     Q = Q.contiguous()
     items = items.contiguous()
     B = user_rows.numel() if user_rows is not None else Q.shape[0]

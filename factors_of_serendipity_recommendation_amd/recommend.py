@@ -19,7 +19,8 @@ may produce.
 from __future__ import annotations
 
 import os
-from typing import Dict, List, Optional, Sequence, Tuple
+from collections.abc import Mapping, Sequence
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -157,14 +158,26 @@ def elasticity_item(mat_candidate: Dict[int, List[int]], dataset_name: str, seed
     np.save(os.path.join(out_dir, "rec_ela.npy"), ragged_topk(key, indptr, items, K))
 
 
+def legacy_float16_bounds(max16: float, min16: float, num_fold: int, epsilon: float) -> Tuple[float, float]:
+    """(min_dis, inter) of recommend.py:377-381 under the numpy the reference pins (1.19.5,
+    environment.yml:253; 1.22.3 at :140), i.e. legacy value-based promotion, not NEP 50:
+      np.max(mat_dis) + epsilon   float16 scalar + Python float -> float64
+      (max_dis - min_dis) / num_fold                             -> float64
+      (mat_dis - min_dis) / inter  float16 array / float64 scalar -> float16 loop: inter is
+                                   rounded to float16 once, here.
+    numpy >= 2 (NEP 50) would round max_dis and inter to float16 step by step instead and move
+    every label boundary by an ulp for about a third of (max, min) pairs."""
+    mx16, mn16 = np.float16(max16), np.float16(min16)
+    inter = (float(mx16) + float(epsilon) - float(mn16)) / num_fold   # float64, as numpy 1.x
+    return float(mn16), float(np.float16(inter))
+
+
 def stratification_bounds(emb_user: torch.Tensor, emb_item: torch.Tensor, num_fold: int = 10,
                           epsilon: float = 0.1) -> Tuple[float, float]:
-    """(min_dis, inter) of recommend.py:375-378 in numpy's float16 arithmetic.  The float16 cast is
-    monotone, so the extremes of the cast matrix are the casts of the fp32 extremes (fused kernel)."""
+    """(min_dis, inter16) of recommend.py:375-381.  The float16 cast is monotone, so the extremes
+    of the cast matrix are the casts of the fp32 extremes (computed inside the fused kernel)."""
     mn, mx = similarity_minmax(emb_user, emb_item)
-    max_dis, min_dis = np.float16(mx) + epsilon, np.float16(mn)
-    inter = (max_dis - min_dis) / num_fold
-    return float(min_dis), float(inter)
+    return legacy_float16_bounds(mx, mn, num_fold, epsilon)
 
 
 def fused_labels_eligible(emb_user: torch.Tensor, d: int) -> bool:
@@ -180,6 +193,8 @@ def strat_labels(emb_user: torch.Tensor, emb_item: torch.Tensor, mask_indptr: to
     users: fused (the MFMA epilogue labels the scores; no [U, I] f32 matrix) when the shape allows,
     else lgx_score_dense rows + lgx_strat_labels.  Both give the same bits."""
     from . import _lib
+    ops.require_gpu(emb_user, emb_item, mask_indptr, mask_indices)
+    ops.check_pair(emb_user, emb_item)
     dev = emb_user.device
     U, I = emb_user.shape[0], emb_item.shape[0]
     L = _lib.lib()
@@ -202,83 +217,201 @@ def strat_labels(emb_user: torch.Tensor, emb_item: torch.Tensor, mask_indptr: to
     return labels, hist
 
 
-def stratified_candidates(emb_user: torch.Tensor, emb_item: torch.Tensor, train: Sequence[Sequence[int]],
-                          targets: Sequence[int], num_fold: int = 10, epsilon: float = 0.1, seed: int = 0,
-                          batch: int = 4096, fused: Optional[bool] = None) -> List[List[int]]:
+class CandidateLists(Sequence):
+    """The candidate lists of a stratified_candidates call: row u is picks[u, :counts[u]] of the flat
+    int32 output the GPU wrote, turned into a Python list only when it is read.  Compares equal to
+    a list of lists with the same rows; pickles as a plain list of lists (what the reference
+    pickles to list_res.pickle, recommend.py:434-435)."""
+
+    def __init__(self, picks: np.ndarray, counts: np.ndarray):
+        self.picks, self.counts = picks, counts
+
+    def __len__(self) -> int:
+        return len(self.counts)
+
+    def row(self, u: int) -> np.ndarray:
+        return self.picks[u, :self.counts[u]]
+
+    def __getitem__(self, u):
+        if isinstance(u, slice):
+            return [self[j] for j in range(*u.indices(len(self)))]
+        return self.row(u).tolist()
+
+    def __iter__(self):
+        return (self.row(u).tolist() for u in range(len(self)))
+
+    def __eq__(self, other) -> bool:
+        if isinstance(other, CandidateLists):
+            return len(self) == len(other) and np.array_equal(self.counts, other.counts) and all(
+                np.array_equal(self.row(u), other.row(u)) for u in range(len(self)))
+        try:
+            return len(self) == len(other) and all(a == b for a, b in zip(self, other))
+        except TypeError:
+            return NotImplemented
+
+    def __reduce__(self):
+        return (list, (), None, iter(self))
+
+
+def stratified_candidates(emb_user: torch.Tensor, emb_item: torch.Tensor, train, targets: Sequence[int],
+                          num_fold: int = 10, epsilon: float = 0.1, seed: int = 0, batch: int = 4096,
+                          fused: Optional[bool] = None) -> CandidateLists:
     """Per user, the stratified candidate list of create_candidates_stratification_sub +
     sample_list (recommend.py:314-356): labels and counts by strat_labels (fused into the scoring
-    kernel's epilogue where the shape allows), the per-label random picks by lgx_strat_select."""
+    kernel's epilogue where the shape allows), the per-label random picks by lgx_strat_select.
+
+    ``train`` is a list of per-user train item lists, or a (indptr, indices) CSR pair.  Raises
+    ValueError where the reference's sampling raises: a negative target (DataFrame.sample(n < 0))
+    or a list that sample_list cannot pad to its target (random.sample(lst, k > len(lst)),
+    recommend.py:317).  The per-batch picks are copied into one pinned host array while the GPU
+    works on the next batch; rows become lists only when read (CandidateLists)."""
     from . import _lib
-    dev = emb_user.device
+    dev = torch.device(emb_user.device)
+    ops.require_gpu(emb_user, emb_item)
+    ops.check_pair(emb_user, emb_item)
     U, I = emb_user.shape[0], emb_item.shape[0]
-    min16, inter16 = stratification_bounds(emb_user, emb_item, num_fold, epsilon)
-    mp, mi = ops.lists_to_device_csr(train, dev, sort=True)
-    tgt = torch.as_tensor(np.asarray(targets, dtype=np.int32), device=dev)
-    K = int(max(1, int(tgt.max().item()) if U else 1))
-    out_lists: List[List[int]] = []
-    L = _lib.lib()
-    st = ops._stream_ptr(dev)
-    pin = dev.type == "cuda"
+    tgt_h = np.asarray(targets, dtype=np.int64)
+    if tgt_h.shape != (U,):
+        raise ValueError(f"targets must have one entry per user ({U}), got shape {tgt_h.shape}")
+    if U and tgt_h.min() < 0:
+        raise ValueError(f"negative candidate target {int(tgt_h.min())} (more test items than K_c)")
+    if U and tgt_h.max() > 1024:
+        raise ValueError("at most 1024 candidates per user")
+    with torch.cuda.device(dev):
+        min16, inter16 = stratification_bounds(emb_user, emb_item, num_fold, epsilon)
+        if isinstance(train, tuple):
+            mp, mi = (t.to(dev) for t in train)
+            mi = mi.to(torch.int32)
+        else:
+            mp, mi = ops.lists_to_device_csr(train, dev, sort=True)
+        if mp.numel() != U + 1:
+            raise ValueError(f"train has {mp.numel() - 1} users, emb_user {U}")
+        tgt = torch.as_tensor(tgt_h.astype(np.int32), device=dev)
+        K = int(max(1, int(tgt_h.max()) if U else 1))
+        L = _lib.lib()
+        stream = torch.cuda.current_stream(dev)
+        st = ops._stream_ptr(dev)
+        picks = torch.empty((U, K), dtype=torch.int32, pin_memory=True)
+        counts = torch.empty(U, dtype=torch.int32, pin_memory=True)
+        for b0 in range(0, U, batch):
+            b1 = min(U, b0 + batch)
+            labels, hist = strat_labels(emb_user[b0:b1], emb_item, mp[b0:], mi, min16, inter16, num_fold, fused)
+            out = torch.empty((b1 - b0, K), dtype=torch.int32, device=dev)
+            cnt = torch.empty(b1 - b0, dtype=torch.int32, device=dev)
+            _lib.check(L.lgx_strat_select(labels.data_ptr(), b1 - b0, I, hist.data_ptr(), num_fold + 1,
+                                          tgt[b0:b1].contiguous().data_ptr(),
+                                          (seed * 0x9E3779B97F4A7C15 + b0) % 2 ** 64,
+                                          out.data_ptr(), K, cnt.data_ptr(), st), "lgx_strat_select")
+            # async D2H on the stream the kernels ran on: the copy engine drains batch b while the
+            # next batch's labels run (the allocator keeps `out` alive until the copy is done)
+            picks[b0:b1].copy_(out, non_blocking=True)
+            counts[b0:b1].copy_(cnt, non_blocking=True)
+        done = torch.cuda.Event()
+        done.record(stream)
+    done.synchronize()
+    res = CandidateLists(picks.numpy(), counts.numpy())
+    short = np.flatnonzero(res.counts < tgt_h)
+    if short.size:
+        u = int(short[0])
+        raise ValueError(f"user {u}: {int(res.counts[u])} of {int(tgt_h[u])} candidates -- sample_list cannot pad "
+                         f"(random.sample: sample larger than population, recommend.py:317)")
+    return res
 
-    def unpack(p):
-        # the host's list building for batch b runs while the GPU labels and selects batch b+1
-        ev, o_h, c_h = p
-        ev.synchronize()
-        o, c = o_h.numpy(), c_h.numpy()
-        rows = o.tolist()  # one C call for the whole batch; only short rows get trimmed
-        for j in np.flatnonzero(c < o.shape[1]).tolist():
-            rows[j] = rows[j][:c[j]]
-        out_lists.extend(rows)
 
-    pending = None
-    for b0 in range(0, U, batch):
-        b1 = min(U, b0 + batch)
-        labels, hist = strat_labels(emb_user[b0:b1], emb_item, mp[b0:], mi, min16, inter16, num_fold, fused)
-        out = torch.empty((b1 - b0, K), dtype=torch.int32, device=dev)
-        cnt = torch.empty(b1 - b0, dtype=torch.int32, device=dev)
-        _lib.check(L.lgx_strat_select(labels.data_ptr(), b1 - b0, I, hist.data_ptr(), num_fold + 1,
-                                      tgt[b0:b1].contiguous().data_ptr(), (seed * 0x9E3779B97F4A7C15 + b0) % 2 ** 64,
-                                      out.data_ptr(), K, cnt.data_ptr(), st), "lgx_strat_select")
-        o_h = torch.empty(out.shape, dtype=torch.int32, pin_memory=pin)
-        c_h = torch.empty(cnt.shape, dtype=torch.int32, pin_memory=pin)
-        o_h.copy_(out, non_blocking=pin)
-        c_h.copy_(cnt, non_blocking=pin)
-        ev = torch.cuda.Event() if pin else None
-        if ev is not None:
-            ev.record()
-        if pending is not None:
-            unpack(pending)
-        pending = (ev if ev is not None else _Done(), o_h, c_h)
-    if pending is not None:
-        unpack(pending)
-    return out_lists
+def train_csr(dataset_name: str, n_users: int, data_root: str = "data") -> Tuple[torch.Tensor, torch.Tensor]:
+    """rating_train.csv as a sorted, de-duplicated CSR: row j = the j-th userInd group, as the
+    reference zips mat_label with df_train.groupby("userInd") (recommend.py:372,421-422)."""
+    import pandas as pd
+    df = pd.read_csv(os.path.join(data_root, dataset_name, "rating_train.csv"), usecols=["userInd", "itemInd"])
+    u = df["userInd"].to_numpy(np.int64)
+    it = df["itemInd"].to_numpy(np.int64)
+    key = np.unique((u << 32) | it)                 # sorted by (user, item), duplicates dropped
+    ku = key >> 32
+    users, lens = np.unique(ku, return_counts=True)  # groups in groupby order
+    lens = lens[:n_users]
+    indptr = np.zeros(len(lens) + 1, np.int64)
+    np.cumsum(lens, out=indptr[1:])
+    items = (key[:indptr[-1]] & 0xFFFFFFFF).astype(np.int32)
+    return torch.from_numpy(indptr), torch.from_numpy(items)
 
 
-class _Done:
-    """Event stand-in for a batch whose copies already completed (synchronous, non-CUDA device)."""
+class CandidateDict(Mapping):
+    """create_candidates_stratification's {user: candidates + test items} (recommend.py:444-451)
+    over the flat GPU output: a user's list is built on first access and then kept (so in-place
+    edits of it persist, as with the reference's dict); pickles (np.save) as a plain dict."""
 
-    def synchronize(self) -> None:
-        pass
+    def __init__(self, lists: Sequence[Sequence[int]], tests: Sequence[Sequence[int]]):
+        self._lists, self._tests, self._memo = lists, tests, {}
+
+    def __len__(self) -> int:
+        return len(self._lists)
+
+    def __iter__(self):
+        return iter(range(len(self._lists)))
+
+    def __contains__(self, u) -> bool:
+        return isinstance(u, (int, np.integer)) and 0 <= u < len(self._lists)
+
+    def __getitem__(self, u):
+        if u not in self:
+            raise KeyError(u)
+        u = int(u)
+        got = self._memo.get(u)
+        if got is None:
+            got = self._memo[u] = list(self._lists[u]) + list(self._tests[u])
+        return got
+
+    def __reduce__(self):
+        return (dict, (), None, None, iter(self.items()))
+
+
+def _save_object(path: str, obj) -> None:
+    """np.save(path, obj) as the reference calls it on a dict: a 0-d object array, pickled."""
+    arr = np.empty((), dtype=object)
+    arr[()] = obj
+    np.save(path, arr)
 
 
 def create_candidates_stratification(dataset_name: str, seed: int, K_c: int = 1000, num_fold: int = 10,
-                                     epsilon: float = 0.1, data_root: str = "data", device="cuda") -> Dict[int, List[int]]:
-    """recommend.create_candidates_stratification: per user the stratified sample of K_c - |test|
-    non-train items followed by the user's test items; saved as rec/<seed>/candidate.npy (a pickled
-    dict, as np.save writes it) and returned.  The cache files are not read back (always recomputed)."""
+                                     epsilon: float = 0.1, data_root: str = "data", device="cuda"):
+    """recommend.create_candidates_stratification (recommend.py:359-452): per user the stratified
+    sample of K_c - |test| non-train items followed by the user's test items.
+
+    The reference's caches are honoured as it honours them: rec/<seed>/candidate.npy is returned
+    when it holds one entry per user (:365-368); rec/<seed>/list_res.pickle, when present, replaces
+    the sampling (:436-440) and is written after it (:434-435).  Both are files this function
+    (or the reference) wrote, read back with pickle as the reference reads them.  A user without
+    test items raises KeyError (:426); targets the sampling cannot meet raise ValueError
+    (stratified_candidates).  Returns a CandidateDict (a lazy Mapping over the flat picks) and
+    writes candidate.npy as the reference's plain dict."""
+    import pickle
     import pandas as pd
+    out_dir = os.path.join(data_root, dataset_name, "rec", str(seed))
+    path_candidate = os.path.join(out_dir, "candidate.npy")
+    path_list_res = os.path.join(out_dir, "list_res.pickle")
     emb_item = np.load(os.path.join(data_root, dataset_name, "emb_item.npy"), allow_pickle=False)
     emb_user = np.load(os.path.join(data_root, dataset_name, "emb_user.npy"), allow_pickle=False)
-    eu = torch.from_numpy(np.ascontiguousarray(emb_user, dtype=np.float32)).to(device)
-    ei = torch.from_numpy(np.ascontiguousarray(emb_item, dtype=np.float32)).to(device)
-    U = eu.shape[0]
-    train = train_lists(dataset_name, U, data_root)
+    if os.path.exists(path_candidate):
+        mat_candidate = np.load(path_candidate, allow_pickle=True).item()
+        if emb_user.shape[0] == len(mat_candidate):
+            return mat_candidate
     test = pd.read_csv(os.path.join(data_root, dataset_name, "rating_test.csv")) \
         .groupby("userInd")["itemInd"].apply(list).to_dict()
-    targets = [K_c - len(test.get(u, [])) for u in range(len(train))]
-    cands = stratified_candidates(eu[:len(train)], ei, train, targets, num_fold, epsilon, seed)
-    mat_candidate = {u: c + list(test.get(u, [])) for u, c in enumerate(cands)}
-    out_dir = os.path.join(data_root, dataset_name, "rec", str(seed))
+    if not os.path.exists(path_list_res):
+        train = train_csr(dataset_name, emb_user.shape[0], data_root)
+        n = train[0].numel() - 1
+        targets = [K_c - len(test[u]) for u in range(n)]             # KeyError as at :426
+        eu = torch.from_numpy(np.ascontiguousarray(emb_user[:n], dtype=np.float32)).to(device)
+        ei = torch.from_numpy(np.ascontiguousarray(emb_item, dtype=np.float32)).to(device)
+        list_res = stratified_candidates(eu, ei, train, targets, num_fold, epsilon, seed)
+        os.makedirs(out_dir, exist_ok=True)
+        with open(path_list_res, "wb") as f:
+            pickle.dump(list_res, f)
+    else:
+        with open(path_list_res, "rb") as f:
+            list_res = pickle.load(f)
+    tests = [test[u] for u in range(len(list_res))]                 # KeyError as at :450
+    mat_candidate = CandidateDict(list_res, tests)
     os.makedirs(out_dir, exist_ok=True)
-    np.save(os.path.join(out_dir, "candidate.npy"), mat_candidate)
+    _save_object(path_candidate, mat_candidate)
     return mat_candidate

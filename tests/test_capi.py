@@ -95,16 +95,17 @@ def test_stratification_rejects_bad_arguments_before_device_work():
 
 
 @pytest.mark.parametrize("mn,mx,num_fold", [(-0.731, 1.42, 10), (0.0, 3.0, 10), (-4.5, 2.25, 7), (-1e-3, 1e-3, 10),
-                                            (-20.0, 35.5, 31)])
+                                            (-20.0, 35.5, 31), (-12.97, 9.34, 10)])
 def test_strat_thresholds_reproduce_float16_labels(mn, mx, num_fold):
     """Host only: lgx_strat_thresholds' step function == numpy's float16 label arithmetic
-    (recommend.py:375-381: (f16(s) - min16) / inter16, floored, every operation rounded to half) on
-    random scores, on every threshold and on its f32 neighbours."""
+    (recommend.py:375-381: (f16(s) - min16) / inter16, floored, the division in the float16 loop)
+    on random scores, on every threshold and on its f32 neighbours.  inter16 as the reference's
+    pinned numpy forms it (legacy promotion, recommend.legacy_float16_bounds)."""
     import numpy as np
-    from factors_of_serendipity_recommendation_amd import _lib
+    from factors_of_serendipity_recommendation_amd import _lib, recommend
     L = _lib.lib()
-    min16 = np.float16(mn)
-    inter16 = (np.float16(mx) + np.float16(0.1) - min16) / np.float16(num_fold)
+    m, i16 = recommend.legacy_float16_bounds(mx, mn, num_fold, 0.1)
+    min16, inter16 = np.float16(m), np.float16(i16)
     thr = (ctypes.c_float * num_fold)()
     assert L.lgx_strat_thresholds(float(min16), float(inter16), num_fold, thr) == 0
     t = np.array(thr[:], dtype=np.float32)

@@ -116,3 +116,12 @@ def test_shard_from_edges_equals_cut_of_full_operator(world):
         for x, y in ((a.A_pull, b.A_pull), (a.A_push, b.A_push)):
             assert torch.equal(x.indptr, y.indptr) and torch.equal(x.indices, y.indices)
             assert torch.equal(x.vals, y.vals)
+
+
+def test_shard_from_edges_rejects_duplicate_or_unsorted_edges():
+    from factors_of_serendipity_recommendation_amd.distributed import make_shard_from_edges
+    u = torch.tensor([0, 0, 1, 2], dtype=torch.int32)
+    for items in ([1, 1, 0, 3], [2, 1, 0, 3]):  # a repeated edge; items out of order within user 0
+        with pytest.raises(ValueError):
+            make_shard_from_edges(u, torch.tensor(items, dtype=torch.int32), 3, 4, 0, 1, seg_len=16)
+    make_shard_from_edges(u, torch.tensor([1, 2, 0, 3], dtype=torch.int32), 3, 4, 0, 1, seg_len=16)

@@ -1,6 +1,8 @@
 """GPU: the multi-GPU propagation schedule with the REAL HIP layer kernels.  The box has one GPU,
-so the two ranks share cuda:0 and exchange over gloo (RCCL refuses two ranks on one device); the
-8-GPU RCCL run is the bench's job.  Checked against the float64 oracle (fp32 tolerance)."""
+so the two ranks share cuda:0 and exchange over gloo (RCCL refuses two ranks on one device); a
+world-1 RCCL group with the collectives forced on runs the async reduce-scatter / all-gather
+stream ordering on the device; the 8-GPU RCCL run is the bench's job.  Checked against the
+float64 oracle (fp32 tolerance)."""
 import os
 import socket
 
@@ -21,10 +23,15 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, K, dtype_name, q):
+def _worker(rank, world, port, K, dtype_name, q, backend="gloo"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+        dist.init_process_group(backend, rank=rank, world_size=world, device_id=torch.device("cuda:0"))
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
     try:
         from oracle import oracle
         import factors_of_serendipity_recommendation_amd as lgx
@@ -39,7 +46,10 @@ def _worker(rank, world, port, K, dtype_name, q):
         if dtype == torch.bfloat16:
             E0 = E0.to(torch.bfloat16).float()
         shard = make_shard(A, U, I, rank, world, seg_len=64)
-        prop = ShardedPropagation(shard, E0[:U].cuda().to(dtype), E0[U:].cuda().to(dtype), K)
+        prop = ShardedPropagation(shard, E0[:U].cuda().to(dtype), E0[U:].cuda().to(dtype), K,
+                                  force_collectives=backend == "nccl")
+        if backend == "nccl":
+            assert prop._collective and prop._rs_native  # async reduce_scatter_tensor / all_gather_into_tensor
         prop.step()
         prop.step()
         ou, oi = prop.gather_outputs()
@@ -73,3 +83,17 @@ def test_sharded_propagation_real_kernels(world, K, dt):
         p.join(timeout=120)
     assert ok, info
     assert all(p.exitcode == 0 for p in procs)
+
+
+@pytest.mark.parametrize("K,dt", [(3, "f32"), (3, "bf16")])
+def test_sharded_propagation_world1_rccl_forced_collectives(K, dt):
+    """One rank, backend "nccl" (RCCL): the reduce-scatter and all-gather are issued as async RCCL
+    collectives on their own stream (the world>1 code path), not the world-1 copies."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(0, 1, _free_port(), K, dt, q, "nccl"))
+    p.start()
+    ok, info = q.get(timeout=300)
+    p.join(timeout=120)
+    assert ok, info
+    assert p.exitcode == 0

@@ -626,3 +626,69 @@ def test_similarity_minmax():
     mn, mx = recommend.similarity_minmax(torch.from_numpy(eu).to(DEV), torch.from_numpy(ei).to(DEV))
     omn, omx = oracle.similarity_minmax(eu, ei)
     assert abs(mn - omn) <= 1e-5 * abs(omn) and abs(mx - omx) <= 1e-5 * abs(omx)
+
+
+@pytest.mark.parametrize("flag", [0, 1])
+def test_batch_test_both_flags_vs_oracle(mlls, flag):
+    """evaluator.batch_test == oracle.batch_test (batch_test.py:25-84) on the mlls KAT inputs, with
+    train_set_flag 0 (mask train, truth = test) and 1 (no mask, truth = train items, :66-68), Ks
+    unsorted as the reference allows; over 2 of its 1024-user batches' worth of repeated users."""
+    U, I = int(mlls["n_users"]), int(mlls["n_items"])
+    A = lgx.build_norm_adj(mlls["train_users"], mlls["train_items"], U, I, dedup=True, device=DEV)
+    E0 = torch.from_numpy(np.concatenate([mlls["emb_user"], mlls["emb_item"]])).to(DEV)
+    out = lgx.propagate(A, E0, 4)
+    tp, tx = mlls["train_list_indptr"], mlls["train_list_indices"]
+    train = {int(u): list(tx[tp[j]:tp[j + 1]]) for j, u in enumerate(mlls["train_list_users"])}
+    sp_, sx = mlls["test_indptr"], mlls["test_indices"]
+    test = {int(u): list(sx[sp_[j]:sp_[j + 1]]) for j, u in enumerate(mlls["test_users"])}
+    users = [int(u) for u in mlls["test_users"]] * 3
+    Ks = [50, 20, 5]
+    got = evaluator.batch_test(out[:U], out[U:], users, train, test, Ks=Ks, train_set_flag=flag)
+    o = out.cpu().numpy()
+    ref = oracle.batch_test(o[:U], o[U:], users, train, test, Ks=Ks, train_set_flag=flag)
+    for key in ("precision", "recall", "ndcg"):
+        # the GPU f32 scores vs the oracle's f64-rounded ones can swap a near-tie (SURVEY 8(a)(ii))
+        assert np.allclose(got[key], ref[key], rtol=0, atol=2e-4), (key, got[key], ref[key])
+    if flag == 1:
+        assert got["precision"][0] > 0.3  # the train items rank first without a mask
+
+
+def test_a_split_folds_into_lightgcn(mlls, tmp_path):
+    """Loader(A_split=True).getSparseGraph() returns A_n_fold row folds (dataloader.py:319-329, the
+    last fold takes the remainder); stacked they are the unsplit coalesced COO.  A dataset that hands
+    LightGCN only the folds (no getCSRGraph) propagates exactly as the unsplit Loader does
+    (model.py:164-168 runs one sparse mm per fold and concatenates)."""
+    from factors_of_serendipity_recommendation_amd.dataloader import Loader
+    from factors_of_serendipity_recommendation_amd.model import LightGCN
+    tp, tx = mlls["train_list_indptr"], mlls["train_list_indices"]
+    with open(tmp_path / "train.txt", "w") as f:
+        for j, u in enumerate(mlls["train_list_users"]):
+            f.write(" ".join(str(x) for x in [u] + list(tx[tp[j]:tp[j + 1]])) + "\n")
+    sp_, sx = mlls["test_indptr"], mlls["test_indices"]
+    with open(tmp_path / "test.txt", "w") as f:
+        for j, u in enumerate(mlls["test_users"]):
+            f.write(" ".join(str(x) for x in [u] + list(sx[sp_[j]:sp_[j + 1]])) + "\n")
+    whole = Loader(path=str(tmp_path), device=DEV, cache_adj=False)
+    split = Loader(config={"A_split": True, "A_n_fold": 7}, path=str(tmp_path), device=DEV, cache_adj=False)
+    folds = split.getSparseGraph()
+    N = whole.n_users + whole.m_items
+    assert isinstance(folds, list) and len(folds) == 7
+    assert [g.shape[0] for g in folds] == [N // 7] * 6 + [N - 6 * (N // 7)]
+    G = whole.getSparseGraph()
+    stacked = torch.cat(folds, dim=0).coalesce()
+    assert torch.equal(stacked.indices(), G.indices()) and torch.equal(stacked.values(), G.values())
+
+    class FoldsOnly:  # the reference's BasicDataset surface, graph as folds only
+        n_users, m_items = whole.n_users, whole.m_items
+
+        def getSparseGraph(self):
+            return folds
+
+    cfg = {"latent_dim_rec": 64, "lightGCN_n_layers": 3, "keep_prob": 0.6, "A_split": True, "pretrain": 1,
+           "dropout": 0, "user_emb": mlls["emb_user"], "item_emb": mlls["emb_item"]}
+    a = LightGCN(cfg, FoldsOnly()).to(DEV).eval()
+    b = LightGCN(dict(cfg, A_split=False), whole).to(DEV).eval()
+    with torch.no_grad():
+        ua, ia = a.computer()
+        ub, ib = b.computer()
+    assert torch.equal(ua, ub) and torch.equal(ia, ib)

@@ -94,6 +94,7 @@ def test_c5_scoring_full_sweep_plan_d256():
     B, I, d, k = 256 * (256 + 67), 100_000, 256, 20
     plan = ops.score_topk_plan(B, I, d, torch.bfloat16, k)
     # the bench's 1M-item catalog seeds its full sweep (test_seeded_full_sweep_equals_one_sweep)
+    # the bench's 1M-item catalog is pinned at full size by test_c5_full_catalog_1m_items_bench_plan
     bench = ops.score_topk_plan(1_000_000, 1_000_000, d, torch.bfloat16, k).replace(" (seeded in stages)", "")
     kinds = [p.split(" users")[0] + " " + p.split(") ")[1].split(" n_splits")[0] for p in plan.split("; ")]
     bkinds = [p.split(" users")[0] + " " + p.split(") ")[1].split(" n_splits")[0] for p in bench.split("; ")]
@@ -257,3 +258,83 @@ def test_c3_amazon_full_size_d128_vs_oracle():
     assert (err <= 1e-5 * np.abs(ref) + 1e-6 * float(E0.float().abs().max())).all(), f"fp32 max err {err.max():.3e}"
     out16 = lgx.propagate(A, E0, cfg.K).cpu().numpy()
     assert (np.abs(out16 - ref) <= 2e-2 * np.abs(ref) + 2e-2 * np.sqrt(np.mean(ref ** 2))).all()
+
+
+def _plan_kinds(plan):
+    """Per launch of a plan string: kernel, mode (seeding included) and n_splits; user ranges and
+    tile counts (which scale with the batch) dropped."""
+    out = []
+    for p in plan.split("; "):
+        kernel = p.split(" users")[0]
+        mode = p.split(") ", 1)[1].split(" utiles")[0]
+        out.append(kernel + " " + mode)
+    return out
+
+
+def _masked_topk_check(Q, items, idx, val, mask, sel, k, chunk=250):
+    """sel users against float64 scores on the device, in chunks: k distinct unmasked items, each
+    within 1e-5 of the exact k-th best, values equal to the float64 scores to 1e-5."""
+    indptr, mi = mask
+    items64 = items.double()
+    for c0 in range(0, sel.numel(), chunk):
+        s = sel[c0:c0 + chunk]
+        S = Q[s].double() @ items64.T
+        for j, u in enumerate(s.tolist()):
+            S[j, mi[indptr[u]:indptr[u + 1]].long()] = float("-inf")
+        kth = torch.topk(S, k, dim=1).values[:, -1:]
+        got_idx = idx[s].long()
+        assert (got_idx >= 0).all()
+        got = S.gather(1, got_idx)
+        assert torch.isfinite(got).all(), "a masked item was returned"
+        assert (got >= kth - 1e-5 * kth.abs().clamp(min=1.0)).all()
+        srt = got_idx.sort(1).values
+        assert (srt[:, 1:] != srt[:, :-1]).all()
+        assert torch.allclose(val[s].double(), got, rtol=1e-5, atol=1e-5)
+        del S
+
+
+def test_c5_full_catalog_1m_items_bench_plan():
+    """BASELINE configs[4] at its own catalog: 82,688 users x 1,000,000 items, d=256 bf16, top-20,
+    50 masked items per user.  The launch plan is the bench's (1 M users) launch for launch: the
+    full sweep seeded in stages (7 launches over [0,16384), ..., [524288, 1M)) and the catalog-split
+    tail with 3 splits -- "seeded" included in the comparison.  1,500 users of each launch are
+    checked against float64 scores on the device."""
+    B, I, d, k = 256 * (256 + 67), 1_000_000, 256, 20
+    plan = ops.score_topk_plan(B, I, d, torch.bfloat16, k)
+    bench = ops.score_topk_plan(1_000_000, I, d, torch.bfloat16, k)
+    assert _plan_kinds(plan) == _plan_kinds(bench), (plan, bench)
+    assert "full-sweep (seeded in stages)" in plan and len(_plan_kinds(plan)) == 2
+    g = torch.Generator(device=DEV).manual_seed(55)
+    Q = (torch.randn(B, d, device=DEV, generator=g) / 16).bfloat16()
+    items = (torch.randn(I, d, device=DEV, generator=g) / 16).bfloat16()
+    m = torch.randint(0, I, (B, 50), device=DEV, generator=g).sort(1).values
+    keep = torch.ones_like(m, dtype=torch.bool)
+    keep[:, 1:] = m[:, 1:] != m[:, :-1]
+    indptr = torch.zeros(B + 1, dtype=torch.int64, device=DEV)
+    indptr[1:] = torch.cumsum(keep.sum(1), 0)
+    mask = (indptr, m[keep].to(torch.int32))
+    idx, val = lgx.score_topk(Q, items, k, mask=mask)
+    sel = torch.cat([torch.randint(0, 65536, (1500,), device=DEV, generator=g),
+                     torch.randint(65536, B, (1500,), device=DEV, generator=g)])
+    _masked_topk_check(Q, items, idx, val, mask, sel, k)
+
+
+def test_c5_fp32_scoring_leg_plan_and_values():
+    """The fp32 scoring leg of the bench (the reference's precision, model.py:183): f32 query and
+    item tables through score_topk_kernel<f32>, 16,384 users x 1,000,000 items, d=256, masked,
+    checked against float64 for 1,000 users."""
+    B, I, d, k = 16384, 1_000_000, 256, 20
+    plan = ops.score_topk_plan(B, I, d, torch.float32, k)
+    assert all(p.startswith("score_topk_kernel") for p in plan.split("; ")), plan
+    g = torch.Generator(device=DEV).manual_seed(57)
+    Q = torch.randn(B, d, device=DEV, generator=g) / 16
+    items = torch.randn(I, d, device=DEV, generator=g) / 16
+    m = torch.randint(0, I, (B, 50), device=DEV, generator=g).sort(1).values
+    keep = torch.ones_like(m, dtype=torch.bool)
+    keep[:, 1:] = m[:, 1:] != m[:, :-1]
+    indptr = torch.zeros(B + 1, dtype=torch.int64, device=DEV)
+    indptr[1:] = torch.cumsum(keep.sum(1), 0)
+    mask = (indptr, m[keep].to(torch.int32))
+    idx, val = lgx.score_topk(Q, items, k, mask=mask)
+    sel = torch.randint(0, B, (1000,), device=DEV, generator=g)
+    _masked_topk_check(Q, items, idx, val, mask, sel, k)

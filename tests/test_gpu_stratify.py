@@ -194,3 +194,115 @@ def test_stratified_candidates_pipelined_batches_equal_per_batch_select():
         want.extend(o[j, :c[j]].tolist() for j in range(b1 - b0))
     assert len(got) == len(train)
     assert got == want
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_labels_on_a_pair_where_numpy_versions_disagree(fused):
+    """(max, min) = (9.34, -12.97) in float16: the reference's numpy 1.19 forms inter = 2.242
+    (float64 chain rounded once), numpy 2's NEP 50 chain 2.24.  Scores are exact products, so the
+    GPU labels (fused epilogue and two-step) must equal the legacy-numpy oracle label for label."""
+    from test_host_logic import crafted_extremes
+    eu, ei = crafted_extremes(9.34, -12.97, U=300, I=5000)
+    rng = np.random.default_rng(4)
+    train = [np.sort(rng.choice(5000, 20, replace=False)).tolist() for _ in range(300)]
+    Eu, Ei = torch.from_numpy(eu).to(DEV), torch.from_numpy(ei).to(DEV)
+    min16, inter16 = recommend.stratification_bounds(Eu, Ei, 10, 0.1)
+    assert np.float16(inter16) == np.float16(2.242)
+    rlab, rhist, rmin, rinter = oracle.stratification_labels(eu, ei, train)
+    assert (min16, inter16) == (rmin, rinter)
+    mp, mi = ops.lists_to_device_csr(train, DEV)
+    lab, hist = recommend.strat_labels(Eu, Ei, mp, mi, min16, inter16, 10, fused=fused)
+    assert np.array_equal(lab.cpu().numpy(), rlab)
+    assert np.array_equal(hist.cpu().numpy(), rhist)
+
+
+def _write_dataset(root, eu, ei, train, test):
+    import pandas as pd
+    (root / "s").mkdir(parents=True, exist_ok=True)
+    np.save(root / "s" / "emb_user.npy", eu)
+    np.save(root / "s" / "emb_item.npy", ei)
+    for name, lists in (("rating_train.csv", train), ("rating_test.csv", test)):
+        pd.DataFrame([(u, i) for u, l in enumerate(lists) for i in l], columns=["userInd", "itemInd"]) \
+            .to_csv(root / "s" / name, index=False)
+
+
+def test_create_candidates_honours_the_reference_caches(tmp_path):
+    """recommend.py:365-368: candidate.npy with one entry per user is returned as is; :416-440:
+    list_res.pickle is written by the first call and, when present, replaces the sampling."""
+    import pickle
+    eu, ei, train = _setup(2, U=30, I=2000)
+    rng = np.random.default_rng(9)
+    test = [rng.choice(2000, 3, replace=False).tolist() for _ in range(30)]
+    root = tmp_path / "data"
+    _write_dataset(root, eu, ei, train, test)
+    rec = root / "s" / "rec" / "3"
+    first = recommend.create_candidates_stratification("s", 3, K_c=300, data_root=str(root), device=DEV)
+    assert isinstance(first, recommend.CandidateDict)
+    with open(rec / "list_res.pickle", "rb") as f:
+        list_res = pickle.load(f)
+    assert type(list_res) is list and all(type(r) is list for r in list_res)
+    assert [r + test[u] for u, r in enumerate(list_res)] == [first[u] for u in range(30)]
+    saved = np.load(rec / "candidate.npy", allow_pickle=True).item()
+    assert type(saved) is dict and saved == dict(first)
+    # candidate.npy present with one entry per user -> returned without recomputing
+    np.save(rec / "candidate.npy", {u: [u] for u in range(30)})
+    assert recommend.create_candidates_stratification("s", 3, K_c=300, data_root=str(root), device=DEV) == \
+        {u: [u] for u in range(30)}
+    # wrong length -> ignored; list_res.pickle present -> its lists + the test items
+    np.save(rec / "candidate.npy", {0: [1]})
+    with open(rec / "list_res.pickle", "wb") as f:
+        pickle.dump([[7, 8]] * 30, f)
+    again = recommend.create_candidates_stratification("s", 3, K_c=300, data_root=str(root), device=DEV)
+    assert all(again[u] == [7, 8] + test[u] for u in range(30))
+    assert np.load(rec / "candidate.npy", allow_pickle=True).item() == dict(again)
+
+
+def test_create_candidates_raises_where_the_reference_raises(tmp_path):
+    """KeyError for a user without test items (recommend.py:426); ValueError when K_c - |test| is
+    negative (DataFrame.sample(n < 0)) or more than sample_list can pad (random.sample, :317)."""
+    eu, ei, train = _setup(2, U=10, I=500)
+    rng = np.random.default_rng(1)
+    test = [rng.choice(500, 3, replace=False).tolist() for _ in range(10)]
+    root = tmp_path / "a"
+    _write_dataset(root, eu, ei, train, test[:9] + [[]])
+    with pytest.raises(KeyError):
+        recommend.create_candidates_stratification("s", 1, K_c=50, data_root=str(root), device=DEV)
+    root = tmp_path / "b"
+    _write_dataset(root, eu, ei, train, test)
+    with pytest.raises(ValueError):
+        recommend.create_candidates_stratification("s", 1, K_c=2, data_root=str(root), device=DEV)
+    Eu, Ei = torch.from_numpy(eu).to(DEV), torch.from_numpy(ei).to(DEV)
+    n_free = [500 - len(t) for t in train]
+    with pytest.raises(ValueError, match="sample_list cannot pad"):
+        recommend.stratified_candidates(Eu, Ei, train, [2 * n_free[0] + 1] + [10] * 9)
+    ok = recommend.stratified_candidates(Eu, Ei, train, [2 * n_free[0]] + [10] * 9)
+    assert len(ok[0]) == 2 * n_free[0]
+
+
+def test_stratified_candidates_guards_mismatched_tables():
+    eu, ei, train = _setup(3, U=8, I=300, d=64)
+    Eu = torch.from_numpy(eu).to(DEV)
+    with pytest.raises(TypeError):
+        recommend.stratified_candidates(Eu, torch.from_numpy(ei).to(DEV).bfloat16(), train, [20] * 8)
+    with pytest.raises(ValueError):
+        recommend.stratified_candidates(Eu, torch.from_numpy(ei[:, :32].copy()).to(DEV), train, [20] * 8)
+    mp, mi = ops.lists_to_device_csr(train, DEV)
+    with pytest.raises(ValueError):
+        recommend.strat_labels(Eu, torch.from_numpy(ei[:, :32].copy()).to(DEV), mp, mi, -1.0, 0.2, 10)
+
+
+def test_stratified_candidates_on_a_side_stream_and_csr_input():
+    """Issued under a non-default current stream (the event that guards the host read must be
+    recorded where the copies run) and with the train items as a CSR pair: same lists."""
+    eu, ei, train = _setup(seed=11, U=500, I=3000, d=64)
+    Eu, Ei = torch.from_numpy(eu).to(DEV), torch.from_numpy(ei).to(DEV)
+    targets = [200] * len(train)
+    ref = recommend.stratified_candidates(Eu, Ei, train, targets, seed=4, batch=128)
+    s = torch.cuda.Stream(device=DEV)
+    s.wait_stream(torch.cuda.current_stream(DEV))
+    with torch.cuda.stream(s):
+        side = recommend.stratified_candidates(Eu, Ei, train, targets, seed=4, batch=128)
+    csr = ops.lists_to_device_csr(train, DEV)
+    via_csr = recommend.stratified_candidates(Eu, Ei, csr, targets, seed=4, batch=128)
+    assert side == ref and via_csr == ref
+    assert ref == [list(r) for r in ref] and len(ref) == 500

@@ -179,3 +179,87 @@ def test_bench_measured_traffic_per_call(tmp_path, monkeypatch):
     monkeypatch.setattr(bench, "lib_sha", lambda: "other")
     assert bench.measured_traffic("cfg", "scoring", 1, ks)[0] is None
     assert bench.measured_traffic("cfg", "scoring", 2, ks)[0] is None
+
+
+def crafted_extremes(mx: float, mn: float, U: int = 48, I: int = 4000, d: int = 64, seed: int = 0):
+    """Embeddings whose f32 scores are exact products u0 * i0: user 0 has u0 = 1 and items 0 / 1
+    carry the float16 values of mx / mn, so the score matrix's float16 extremes are exactly them."""
+    rng = np.random.default_rng(seed)
+    mx16, mn16 = np.float32(np.float16(mx)), np.float32(np.float16(mn))
+    eu = np.zeros((U, d), np.float32)
+    ei = np.zeros((I, d), np.float32)
+    eu[:, 0] = rng.uniform(0.05, 1.0, U).astype(np.float32)
+    eu[0, 0] = 1.0
+    ei[:, 0] = rng.uniform(mn16, mx16, I).astype(np.float32)
+    ei[0, 0], ei[1, 0] = mx16, mn16
+    return eu, ei
+
+
+def test_stratification_bounds_follow_the_pinned_numpy():
+    """recommend.py:377-381 under numpy 1.19.5 (environment.yml:253): max_dis and inter are float64
+    and inter is rounded to float16 once, at the division.  (9.34, -12.97) is a pair where numpy 2's
+    NEP 50 chain of float16 roundings gives another inter (2.24 instead of 2.242) and so other
+    labels; the product and the oracle both take the legacy value."""
+    from factors_of_serendipity_recommendation_amd import recommend
+    mx16, mn16 = np.float16(9.34), np.float16(-12.97)
+    legacy = np.float16((float(mx16) + 0.1 - float(mn16)) / 10)        # float64 chain, one rounding
+    nep50 = (mx16 + 0.1 - mn16) / 10                                     # float16 chain (numpy >= 2)
+    assert legacy == np.float16(2.242) and nep50 == np.float16(2.24) and legacy != nep50
+    assert recommend.legacy_float16_bounds(9.34, -12.97, 10, 0.1) == (float(mn16), float(legacy))
+    eu, ei = crafted_extremes(9.34, -12.97)
+    lab, hist, rmin, rinter = oracle.stratification_labels(eu, ei, [[] for _ in range(len(eu))])
+    assert rmin == float(mn16) and rinter == float(legacy)
+    s16 = (eu @ ei.T).astype(np.float16)
+    assert s16.max() == mx16 and s16.min() == mn16
+    assert np.array_equal(lab, np.floor((s16 - mn16) / legacy).astype(np.int8))
+    assert (lab != np.floor((s16 - mn16) / nep50).astype(np.int8)).any()  # the pair discriminates
+
+
+def test_candidate_containers_pickle_as_the_reference_types():
+    """CandidateLists pickles as a list of lists (list_res.pickle), CandidateDict as a dict
+    (candidate.npy); a CandidateDict row is built once and keeps in-place edits."""
+    import pickle
+    from factors_of_serendipity_recommendation_amd.recommend import CandidateDict, CandidateLists, _save_object
+    picks = np.array([[3, 1, 2], [9, 8, 0]], np.int32)
+    lists = CandidateLists(picks, np.array([3, 2], np.int32))
+    assert lists == [[3, 1, 2], [9, 8]] and lists[1] == [9, 8] and lists[0:1] == [[3, 1, 2]]
+    back = pickle.loads(pickle.dumps(lists))
+    assert type(back) is list and back == [[3, 1, 2], [9, 8]]
+    d = CandidateDict(lists, [[5], [6, 7]])
+    assert dict(d) == {0: [3, 1, 2, 5], 1: [9, 8, 6, 7]} and 2 not in d
+    d[0].append(4)
+    assert d[0] == [3, 1, 2, 5, 4]
+    with pytest.raises(KeyError):
+        d[2]
+    back = pickle.loads(pickle.dumps(d))
+    assert type(back) is dict and back == {0: [3, 1, 2, 5, 4], 1: [9, 8, 6, 7]}
+
+
+def test_lists_to_csr_sorts_rows_on_the_device_path():
+    rng = np.random.default_rng(5)
+    lists = [rng.choice(10 ** 6, int(rng.integers(0, 30)), replace=False).tolist() for _ in range(200)]
+    ip, ix = lists_to_device_csr(lists, "cpu")
+    ip, ix = ip.numpy(), ix.numpy()
+    for j, l in enumerate(lists):
+        assert ix[ip[j]:ip[j + 1]].tolist() == sorted(l)
+    with pytest.raises(ValueError):
+        lists_to_device_csr([[1, -2]], "cpu")
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_vectorised_test_one_batch_equals_reference_loops(seed):
+    """evaluator.test_one_batch (one membership search for the batch) == the oracle's restatement
+    of the reference's per-user loops (Procedure.py:60-72, code/utils.py:218-285), bit for bit:
+    ragged truths (1..60 items, duplicates), predictions with hits at any rank, k > |truth|."""
+    from factors_of_serendipity_recommendation_amd.evaluator import test_one_batch
+    rng = np.random.default_rng(seed)
+    n, M = 3000, 5000
+    truth = [rng.integers(0, M, int(rng.integers(1, 60))).tolist() for _ in range(n)]
+    pred = rng.integers(0, M, (n, 100))
+    for i in range(0, n, 3):  # plant hits
+        t = truth[i]
+        pred[i, rng.integers(0, 100, min(len(t), 5))] = t[:min(len(t), 5)]
+    got = test_one_batch(pred, truth, [1, 5, 20, 100])
+    ref = oracle.torch_style_metrics(pred, truth, [1, 5, 20, 100])
+    for key in ("recall", "precision", "ndcg"):
+        assert np.array_equal(got[key], ref[key]), key
