@@ -85,7 +85,12 @@ class _CapturedStep:
     propagation of it) and the Adam step -- captured once as a hipGraph (torch.cuda.CUDAGraph) and
     replayed per minibatch: one host call instead of ~20 launches, so the epoch runs at the GPU's
     pace whatever the host does (the eager loop issues 0.26 ms of launches per 0.31 ms minibatch).
-    Inputs are copied into static index buffers; the loss comes back in a static tensor."""
+    Inputs are copied into static index buffers; the loss comes back in a static tensor.
+
+    A replay repeats the host values and device addresses frozen at capture: lr / betas / eps and
+    the decay factor are kernel scalars, the parameters and the optimizer state tensors are captured
+    by address.  ``key`` records them; a change (an lr schedule, ``opt.load_state_dict`` replacing
+    the state tensors, a new decay) makes the next minibatch re-capture instead of replaying."""
 
     def __init__(self, loss_class, batch_size: int, device):
         self.bs = batch_size
@@ -95,11 +100,28 @@ class _CapturedStep:
         self.graph = None
         self.loss = None
         self.failed = False
+        self.key = None
+        self.captures = 0
+
+    @staticmethod
+    def capture_key(loss_class):
+        opt = loss_class.opt
+        groups = []
+        for g in opt.param_groups:
+            params = []
+            for prm in g["params"]:
+                st = opt.state.get(prm, {})
+                params.append((prm.data_ptr(), tuple(st[k].data_ptr() if torch.is_tensor(st.get(k)) else None
+                                     for k in ("step", "exp_avg", "exp_avg_sq"))))
+            groups.append((float(g["lr"]), tuple(g["betas"]), float(g["eps"]), tuple(params)))
+        return id(opt), float(loss_class.weight_decay), tuple(groups)
 
     def run(self, loss_class, u, p, n):
         self.u.copy_(u)
         self.p.copy_(p)
         self.n.copy_(n)
+        if self.graph is not None and self.capture_key(loss_class) != self.key:
+            self.graph = None  # frozen scalars / addresses changed: capture again
         if self.graph is None:
             dev = self.u.device
             # warm-up = this minibatch's real step, eager on a side stream (allocates the gradients,
@@ -119,6 +141,8 @@ class _CapturedStep:
                 self.failed = True
                 return out
             self.graph = graph
+            self.key = self.capture_key(loss_class)
+            self.captures += 1
             return out
         self.graph.replay()
         return self.loss

@@ -150,7 +150,11 @@ int lgx_layer_epilogue(const float* y, int64_t rows, void* Y, const void* E0, fl
 int lgx_spmm_kernel_name(int64_t d, int dtype, int64_t seg_len, char* buf, size_t len);
 /*
  * The last layer over kept layer tables: out = (E0 + prev[0] + ... + prev[n_prev-1] + A X) / n_mean,
- * summed in that order in fp32 (for fp32 storage the same bits as the FIRST / MID / LAST chain).
+ * summed in that order in fp32.  fp32 storage: the same bits as the FIRST / MID / LAST chain.
+ * bf16 storage: NOT the same bits -- the chain added each layer's unrounded f32 A X to its f32
+ * running sum, the stack adds the bf16-rounded layer tables (one extra bf16 rounding per kept
+ * layer, |rel| <= 2^-9 each).  Pinned against the float64 oracle at the bf16 tolerance
+ * 2e-2 |ref| + 2e-2 rms(ref) (tests/test_gpu_pinned.py, test_gpu_parity.py).
  * prev: host array of n_prev <= 7 device pointers to [n_rows, d] dtype tables (PLAIN outputs).
  * Per layer this moves (n_prev + 1) dtype tables + one f32 table instead of an f32 running sum
  * read and written every layer.
@@ -163,7 +167,8 @@ int lgx_spmm_csr(const lgx_csr* A, const void* X, void* Y, int64_t d, int dtype,
 int lgx_propagate_workspace(int64_t n_rows, int64_t d, int dtype, size_t* ws_bytes);
 /* Whole K-layer propagation (square A, X = E0 table [N,d] dtype) -> out [N,d] f32 layer mean.
  * When the K-1 intermediate tables fit the workspace (bf16: K <= 5, f32: K <= 4) they are kept
- * and the last layer forms the mean (LGX_LAYER_STACK); otherwise the f32 running sum. */
+ * and the last layer forms the mean (LGX_LAYER_STACK); otherwise the f32 running sum.  The two
+ * schedules give identical fp32 results; in bf16 they differ by the rounding noted above. */
 int lgx_propagate(const lgx_csr* A, const void* E0, float* out, int64_t d, int K, int dtype,
                   void* ws, size_t ws_bytes, lgx_stream_t stream);
 

@@ -124,6 +124,41 @@ def test_captured_epoch_equals_eager_epoch(mlls, tmp_path):
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-5 * b.abs().max().item())
 
 
+def test_captured_step_recaptures_on_lr_change_and_state_reload(mlls, tmp_path):
+    """The captured minibatch freezes lr / betas / eps / decay and the optimizer state addresses:
+    a scheduler-style lr change between epochs and an opt.load_state_dict (new state tensors) must
+    re-capture, so the captured run still equals the eager run with the same changes."""
+    import copy
+    from factors_of_serendipity_recommendation_amd.dataloader import Loader
+    from factors_of_serendipity_recommendation_amd.model import LightGCN
+    tp, tx = mlls["train_list_indptr"], mlls["train_list_indices"]
+    with open(tmp_path / "train.txt", "w") as f:
+        for j, u in enumerate(mlls["train_list_users"]):
+            f.write(" ".join(str(x) for x in [u] + list(tx[tp[j]:tp[j + 1]])) + "\n")
+    with open(tmp_path / "test.txt", "w") as f:
+        f.write(f"{int(mlls['train_list_users'][0])} {int(tx[0])}\n")
+    ds = Loader(path=str(tmp_path), device=DEV)
+    cfg = {"latent_dim_rec": 64, "lightGCN_n_layers": 3, "keep_prob": 0.6, "A_split": False, "pretrain": 0,
+           "dropout": 0, "decay": 1e-4, "lr": 0.001}
+    runs = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        model = LightGCN(cfg, ds).to(DEV)
+        bpr = train.BPRLoss(model, cfg)
+        sampling.seed(11)
+        train.BPR_train_original(ds, model, bpr, 0, batch_size=512, device=DEV, graph=graph)
+        for g in bpr.opt.param_groups:
+            g["lr"] = 0.01  # a scheduler step
+        train.BPR_train_original(ds, model, bpr, 1, batch_size=512, device=DEV, graph=graph)
+        bpr.opt.load_state_dict(copy.deepcopy(bpr.opt.state_dict()))  # new state tensors
+        train.BPR_train_original(ds, model, bpr, 2, batch_size=512, device=DEV, graph=graph)
+        if graph:
+            assert bpr._lgx_captured.captures == 3
+        runs.append([p.detach().clone() for p in model.parameters()])
+    for a, b in zip(*runs):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-5 * b.abs().max().item())
+
+
 # ---------------------------------------------------------------- fused BPR loss (csrc/bpr.hip)
 def _torch_bpr(light, wu, wi, users, pos, neg):
     """model.py:196-209 in the reference's torch ops (fp32), the parity reference."""
