@@ -347,8 +347,8 @@ def cpu_baseline(A, E0, cfg, target_nnz):
 
 def bench_scoring(args, rank, world, dtype, B_total, steps, with_cpu):
     """configs[4]: d=256, 1M items, top-20 with a 50-item train mask; users split over ranks.
-    dtype float32 = the reference's precision (model.py:183 fp32 matmul; score_topk_kernel<f32>,
-    v_mfma_f32_32x32x2_f32, against the 157.3 TF f32 MFMA peak); bfloat16 = SURVEY C5's inputs
+    dtype float32 = the reference's precision (model.py:183 fp32 matmul; score_topk_f32_lds,
+    v_mfma_f32_16x16x4_f32, against the 157.3 TF f32 MFMA peak); bfloat16 = SURVEY C5's inputs
     (score_topk_bf16_lds, against 2.5 PF)."""
     d, n_items, k = 256, args.score_items, 20
     B = B_total // world
@@ -378,7 +378,7 @@ def bench_scoring(args, rank, world, dtype, B_total, steps, with_cpu):
     flops = 2.0 * B * n_items * d
     plan = ops.score_topk_plan(B, n_items, d, dtype, k)
     peak = F32_MFMA_PEAK if f32 else BF16_MFMA_PEAK
-    sweep = "score_topk_kernel" if f32 else "score_topk_bf16_lds"
+    sweep = plan.split("<", 1)[0]  # the sweep kernel the plan launches (score_topk_f32_lds / _bf16_lds)
     # per lgx_score_topk call: every stage of every user range (finalize runs once per range)
     traffic, tsrc = measured_traffic(args.config, "scoring_f32" if f32 else "scoring", world,
                                      [sweep, "score_topk_finalize"],
@@ -393,8 +393,7 @@ def bench_scoring(args, rank, world, dtype, B_total, steps, with_cpu):
                          "unit": "TFLOP/s", "frac": flops / mean_launch / peak, "traffic": traffic,
                          "traffic_unit": "GB/call", "traffic_source": tsrc,
                          "kernel": f"{sweep} (+ score_topk_finalize, both inside the timed launch)",
-                         "launch": "one lgx_score_topk call: " + ("its seeded stages and split tail" if not f32
-                                                                  else "its catalog-split launches")},
+                         "launch": "one lgx_score_topk call: every launch of its plan (seeded stages, split tail)"},
             "cpu_baseline": cpu}
 
 

@@ -738,11 +738,11 @@ __global__ __launch_bounds__(WPB * 64) void score_topk_kernel(ScoreArgs a) {
 // Workgroup shape: WAVES x 32 users, tiles of 32*NACC items.  <8, 2> (one 512-thread workgroup per
 // CU, 64-item tiles) is the one launched; see lds_waves() for the measured alternative.
 
-template <int KSTEPS, int WAVES = 8, int NACC = 2>
+template <int KSTEPS, int WAVES = 8, int NACC = 2, int ESZ = 2>
 struct LdsGeom {
     static constexpr int TILE_ITEMS = 32 * NACC;
     static constexpr int USERS = WAVES * kUsersPerWave;
-    static constexpr int RB = KSTEPS * 32;              // bytes per bf16 item row (d = 16*KSTEPS)
+    static constexpr int RB = KSTEPS * 16 * ESZ;        // bytes per item row (d = 16*KSTEPS, ESZ-byte elements)
     static constexpr int CPR = RB / 16;                 // 16-B chunks per row
     static constexpr int TILE = TILE_ITEMS * RB;        // bytes per tile
     static constexpr int PIECES = TILE / 1024;          // 1-KiB LDS-DMA wave instructions per tile
@@ -805,19 +805,31 @@ __device__ __forceinline__ uint32_t lds_u32(const void* p) {
 #ifndef LGX_DIRECT_EVENTS  // development A/B: -DLGX_DIRECT_EVENTS=0 keeps the regroup-always event path
 #define LGX_DIRECT_EVENTS 1
 #endif
-template <int KSTEPS, bool MINMAX, int ABLATE = 0, int WAVES = 8, int NACC = 2, bool STAGGER = true, bool M16 = true,
-          int DMAPOS = 0, bool FASTSKIP = true>
-__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
-void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf) {
-    static_assert(!M16 || (NACC == 2 && KSTEPS % 2 == 0), "16x16x32 path: 64-item tiles, d a multiple of 32");
+//
+// fp32 (DT = LGX_DTYPE_F32, score_topk_f32_lds): the same walk on v_mfma_f32_16x16x4_f32 (exact f32
+// products and sums, the reference's precision).  A 16-B chunk of a row now holds 4 features, and
+// the MFMA's k index q4 = lane >> 4 takes feature 16 s + 4 q4 + e at step (s, e): the same chunk
+// (4 s + q4) of the item row and of the user row as the bf16 walk reads, so the LDS ring, the
+// swizzle and the accumulator layout (hence the whole top-k epilogue) are shared.  At 1/16 of the
+// bf16 MFMA rate a 64-item tile is 16 K MFMA cycles per wave, so the workgroup is 4 waves x 32 users,
+// ONE wave per SIMD with the full 512-register file (the 32 users' f32 rows take 128 VGPRs), no
+// stagger (no partner wave to overlap), a 2-buffer ring of 64 KB tiles at d = 256.
+template <int DT, int KSTEPS, bool MINMAX, int ABLATE, int WAVES, int NACC, bool STAGGER, bool M16, int DMAPOS,
+          bool FASTSKIP>
+__device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreArgs a, int xcd_affine,
+                                                    int64_t n_utiles, int nbuf) {
+    constexpr bool F32 = DT == LGX_DTYPE_F32;
+    static_assert(!M16 || (NACC == 2 && (F32 || KSTEPS % 2 == 0)), "16x16 path: 64-item tiles, bf16 d a multiple of 32");
+    static_assert(!F32 || M16, "fp32: the 16x16x4 walk only");
     // SKIP: the fast-path test runs on the MFMA output layout itself (lane l holds 16 scores of user
     // l & 15 and 16 of user 16 + (l & 15)); the regroup into the top-k layout (16 v_permlane16_swap)
     // is paid only by tiles that have a survivor.  Min / max needs every score: not with MINMAX.
     constexpr bool SKIP = FASTSKIP && M16 && !MINMAX && (ABLATE == 0 || ABLATE == 9);
     constexpr bool DIRECT_EVENTS = LGX_DIRECT_EVENTS != 0;
-    typedef LdsGeom<KSTEPS, WAVES, NACC> G;
-    typedef Frag<LGX_DTYPE_BF16> F;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    typedef LdsGeom<KSTEPS, WAVES, NACC, F32 ? 4 : 2> G;
+    typedef Frag<DT> F;
+    constexpr int NS = G::CPR / 4;                  // 16x16 walk: chunk groups (k-steps of 4 chunks) per row
+    constexpr int UFN = M16 ? 2 * NS : KSTEPS;      // user fragment registers (16 B each)
     unsigned char* tiles = smem;  // [nbuf][TILE]
     const int k = a.k;
     const int lane = threadIdx.x & 63;
@@ -842,22 +854,22 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
 
     const int64_t b = utile * G::USERS + wave * kUsersPerWave + col;
     const bool user_ok = b < a.B;
-    typename F::chunk uf[KSTEPS];
+    uint4 uf[UFN];
     const int r16 = lane & 15, q4 = lane >> 4;
-    if (M16) {  // B fragment (ub, s) at uf[ub * KSTEPS / 2 + s]: user 16 ub + r16, features 32 s + 8 q4
+    if (M16) {  // B fragment (ub, s) at uf[ub * NS + s]: user 16 ub + r16, 16-B chunk 4 s + q4 of its row
 #pragma unroll
         for (int ub = 0; ub < 2; ++ub) {
             const int64_t bu = utile * G::USERS + wave * kUsersPerWave + 16 * ub + r16;
             const bool ok = bu < a.B;
             const int64_t qr = ok ? (a.user_rows ? a.user_rows[bu] : bu) : 0;
 #pragma unroll
-            for (int s2 = 0; s2 < KSTEPS / 2; ++s2)
-                uf[ub * (KSTEPS / 2) + s2] = F::load(a.Q, qr, a.d, 2 * s2 + (q4 >> 1), q4 & 1, ok);
+            for (int s2 = 0; s2 < NS; ++s2)
+                uf[ub * NS + s2] = __builtin_bit_cast(uint4, F::load(a.Q, qr, a.d, 2 * s2 + (q4 >> 1), q4 & 1, ok));
         }
     } else {
         const int64_t qrow = user_ok ? (a.user_rows ? a.user_rows[b] : b) : 0;
 #pragma unroll
-        for (int c = 0; c < KSTEPS; ++c) uf[c] = F::load(a.Q, qrow, a.d, c, h, user_ok);
+        for (int c = 0; c < KSTEPS; ++c) uf[c] = __builtin_bit_cast(uint4, F::load(a.Q, qrow, a.d, c, h, user_ok));
     }
     WaveTopK st;
     st.init(lk, lk + list_keys_per_wave(k), k, lane, b, user_ok);
@@ -867,7 +879,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
     // consume the prologue loads here: otherwise the compiler treats them as possibly pending at
     // the loop header and waits vmcnt(0) -- i.e. for the tile prefetch -- in every iteration
 #pragma unroll
-    for (int c = 0; c < KSTEPS; ++c) {
+    for (int c = 0; c < UFN; ++c) {
         u32x4 t = __builtin_bit_cast(u32x4, uf[c]);
         asm volatile("" : "+v"(t));
         uf[c] = __builtin_bit_cast(uint4, t);
@@ -968,7 +980,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
     auto compute = [&]() {
         const unsigned char* T = tiles + buf * G::TILE;
         if constexpr (M16) {
-            constexpr int KS2 = KSTEPS / 2;
+            constexpr int KS2 = NS;
 #pragma unroll
             for (int ub = 0; ub < 2; ++ub)
 #pragma unroll
@@ -988,10 +1000,20 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
 #pragma unroll
                 for (int ib = 0; ib < 4; ++ib) {
 #pragma unroll
-                    for (int ub = 0; ub < 2; ++ub)
-                        c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                            __builtin_bit_cast(bf16x8, fa[ib]), __builtin_bit_cast(bf16x8, uf[ub * KS2 + s2]),
-                            c[ub][ib], 0, 0, 0);
+                    for (int ub = 0; ub < 2; ++ub) {
+                        if constexpr (F32) {
+                            const float4 av = __builtin_bit_cast(float4, fa[ib]);
+                            const float4 bv = __builtin_bit_cast(float4, uf[ub * KS2 + s2]);
+                            c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, c[ub][ib], 0, 0, 0);
+                            c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, c[ub][ib], 0, 0, 0);
+                            c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, c[ub][ib], 0, 0, 0);
+                            c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, c[ub][ib], 0, 0, 0);
+                        } else {
+                            c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                __builtin_bit_cast(bf16x8, fa[ib]), __builtin_bit_cast(bf16x8, uf[ub * KS2 + s2]),
+                                c[ub][ib], 0, 0, 0);
+                        }
+                    }
                     if (s2 + 1 < KS2 && ABLATE != 8) fa[ib] = frag(s2 + 1, ib);  // 8 (development): one read per tile
                 }
                 if (DMAPOS == 1 && s2 < G::PPW && refill) stage_piece(sbuf, refill_t0, s2);
@@ -1001,7 +1023,7 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
             for (int s2 = 0; s2 < KS2; ++s2) {
 #pragma unroll
                 for (int ib = 0; ib < 4; ++ib) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, F32 ? 8 : 2, 0);
                     if (s2 + 1 < KS2) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 }
             }
@@ -1161,6 +1183,24 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
 #ifdef LGX_SCORE_STATS
     { uint64_t* stat_ = st.stat_; LGX_STAT_FLUSH }
 #endif
+}
+
+template <int KSTEPS, bool MINMAX, int ABLATE = 0, int WAVES = 8, int NACC = 2, bool STAGGER = true, bool M16 = true,
+          int DMAPOS = 0, bool FASTSKIP = true>
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    score_topk_lds_body<LGX_DTYPE_BF16, KSTEPS, MINMAX, ABLATE, WAVES, NACC, STAGGER, M16, DMAPOS, FASTSKIP>(
+        smem, a, xcd_affine, n_utiles, nbuf);
+}
+
+constexpr int kF32LdsWaves = 4;
+template <int KSTEPS, bool MINMAX>
+__global__ __launch_bounds__(kF32LdsWaves * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void score_topk_f32_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    score_topk_lds_body<LGX_DTYPE_F32, KSTEPS, MINMAX, 0, kF32LdsWaves, 2, false, true, 0, true>(
+        smem, a, xcd_affine, n_utiles, nbuf);
 }
 
 // one wave per query: merge the split lists, masked tail, optional sigmoid (k <= 64 R)
@@ -1576,30 +1616,37 @@ __global__ __launch_bounds__(kDenseWaves * 64) void strat_label_lds(const void* 
 struct SplitPlan {
     int n_splits;
     int64_t split_items;
-    bool lds;        // bf16 LDS-DMA kernel
+    bool lds;        // LDS-DMA kernel (score_topk_bf16_lds / score_topk_f32_lds)
     bool xcd_affine;
     int64_t n_utiles;
-    int waves;       // LDS kernel shape: 4 (two workgroups per CU, 32-item tiles) or 8 (one, 64-item)
+    int waves;       // LDS kernel workgroup: 8 waves (bf16, two per SIMD) or 4 (f32, one per SIMD)
 };
 
-// LDS kernel shape.  The two-workgroups-per-CU shape <4, 1> was measured slower (902 vs 1079 TF/s
-// unmasked, 131072 users, d=256): halving the tile doubles the barriers per MFMA, which costs more
-// than the overlap of two independent workgroups recovers.  Only <8, 2> is instantiated.
-inline int lds_waves() { return 8; }
-inline int64_t lds_resident(int waves) { return waves == 4 ? 512 : 256; }  // workgroups at once
+// LDS kernel shape.  bf16: <8 waves, 64-item tiles>, one workgroup per CU; the two-workgroups-per-CU
+// shape <4, 1> was measured slower (902 vs 1079 TF/s unmasked, 131072 users, d=256): halving the tile
+// doubles the barriers per MFMA, which costs more than the overlap of two independent workgroups
+// recovers.  f32: <4 waves, 64-item tiles>, one workgroup (one wave per SIMD) per CU.  Either way one
+// workgroup per CU, 256 resident.
+inline int lds_waves(int dtype) { return dtype == LGX_DTYPE_F32 ? kF32LdsWaves : 8; }
+inline int64_t lds_resident() { return 256; }
 
-// LDS kernel applies to bf16, d a multiple of 32 up to 256 (even k-step counts are instantiated),
-// k <= 32 (LDS budget)
+constexpr size_t kLdsBytes = 160 * 1024;
+constexpr int kTileItems = 64;
+// LDS kernel applies to bf16 with d a multiple of 32 up to 256 (even k-step counts are
+// instantiated) and k <= 32; to f32 with d a multiple of 64 up to 256 when two 64-item tiles fit
+// beside the 4 waves' top-k lists (d = 256: k <= 20)
 bool lds_eligible(int dtype, int64_t d, int k) {
-    return dtype == LGX_DTYPE_BF16 && d % 32 == 0 && d >= 32 && d <= 256 && k <= 32;
+    if (dtype == LGX_DTYPE_BF16) return d % 32 == 0 && d >= 32 && d <= 256 && k <= 32;
+    if (dtype != LGX_DTYPE_F32 || d % 64 != 0 || d < 64 || d > 256 || k > 32) return false;
+    return 2 * (size_t)kTileItems * d * 4 + (size_t)kF32LdsWaves * list_bytes_per_wave(k) <= kLdsBytes;
 }
 
 SplitPlan plan_splits(int64_t B, int64_t n_items, int dtype, int64_t d, int k) {
     const int64_t tiles32 = ceil_div(n_items, 32);
     if (lds_eligible(dtype, d, k)) {
-        const int waves = lds_waves();
-        const int64_t users = waves * kUsersPerWave, tile_items = waves == 4 ? 32 : 64;
-        const int64_t resident = lds_resident(waves);
+        const int waves = lds_waves(dtype);
+        const int64_t users = waves * kUsersPerWave, tile_items = kTileItems;
+        const int64_t resident = lds_resident();
         const int64_t ut = ceil_div(B, users);
         const int64_t tiles = ceil_div(n_items, tile_items);
         // a full round or more: no catalog split -- every split repeats the list-filling phase, which
@@ -1668,7 +1715,6 @@ int launch_v1(const ScoreArgs& a, int kch, hipStream_t stream) {
 
 // tile buffers of the LDS kernel: as many as fit beside the top-k lists in the workgroup's share of
 // the CU's LDS, 2..4
-constexpr size_t kLdsBytes = 160 * 1024;
 inline int lds_ring_buffers(size_t tile, size_t lists, int wg_per_cu) {
     const size_t budget = kLdsBytes / wg_per_cu;
     const size_t fit = lists < budget ? (budget - lists) / tile : 0;
@@ -1679,7 +1725,7 @@ template <int KS, bool MM, int ABL, int WAVES, int NACC, bool STAGGER, bool M16,
 int launch_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     typedef LdsGeom<KS, WAVES, NACC> G;
     const size_t lists = (size_t)WAVES * list_bytes_per_wave(a.k);
-    const int nbuf = lds_ring_buffers(G::TILE, lists, WAVES == 4 ? 2 : 1);
+    const int nbuf = lds_ring_buffers(G::TILE, lists, 1);
     const size_t shmem = (size_t)nbuf * G::TILE + lists;
     int rc = set_lds_limit(score_topk_bf16_lds<KS, MM, ABL, WAVES, NACC, STAGGER, M16, DMAPOS, SKIP>, shmem);
     if (rc) return rc;
@@ -1705,9 +1751,40 @@ int launch_lds_shape(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream)
     return launch_lds_kernel<KS, MM, ABL, WAVES, NACC, true, true>(a, p, stream);
 }
 
+template <int KS, bool MM>
+int launch_f32_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
+    typedef LdsGeom<KS, kF32LdsWaves, 2, 4> G;
+    const size_t lists = (size_t)kF32LdsWaves * list_bytes_per_wave(a.k);
+    const int nbuf = lds_ring_buffers(G::TILE, lists, 1);
+    const size_t shmem = (size_t)nbuf * G::TILE + lists;
+    if (shmem > kLdsBytes) {
+        set_error("lgx_score_topk: f32 LDS kernel needs %zu B of LDS", shmem);
+        return LGX_ERR_UNSUPPORTED;
+    }
+    int rc = set_lds_limit(score_topk_f32_lds<KS, MM>, shmem);
+    if (rc) return rc;
+    const unsigned grid = (unsigned)(p.n_utiles * p.n_splits);
+    score_topk_f32_lds<KS, MM><<<grid, kF32LdsWaves * 64, shmem, stream>>>(a, p.xcd_affine ? 1 : 0, p.n_utiles, nbuf);
+    LGX_LAUNCH_CHECK();
+    return LGX_OK;
+}
+
 template <bool MM, int ABL = 0>
-int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
+int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream, int dtype = LGX_DTYPE_BF16) {
     const int ksteps = (int)(a.d / 16);
+    if constexpr (ABL == 0) {
+        if (dtype == LGX_DTYPE_F32) {
+            switch (ksteps) {
+                case 4: return launch_f32_lds_kernel<4, MM>(a, p, stream);
+                case 8: return launch_f32_lds_kernel<8, MM>(a, p, stream);
+                case 12: return launch_f32_lds_kernel<12, MM>(a, p, stream);
+                case 16: return launch_f32_lds_kernel<16, MM>(a, p, stream);
+                default:
+                    set_error("lgx_score_topk: no f32 LDS kernel for d=%lld", (long long)a.d);
+                    return LGX_ERR_UNSUPPORTED;
+            }
+        }
+    }
     if constexpr (ABL != 0) {  // development ablations: d = 256 only
         if (ksteps != 16) {
             set_error("lgx_score_topk: ablation builds exist for d=256 only");
@@ -1752,7 +1829,7 @@ int plan_ranges(int64_t B, int64_t n_items, int dtype, int64_t d, int k, UserRan
     const SplitPlan p = plan_splits(B, n_items, dtype, d, k);
     int n = 0;
     int64_t full = B;
-    const int64_t resident = lds_resident(p.waves);
+    const int64_t resident = lds_resident();
     if (p.lds && p.n_splits == 1 && p.n_utiles >= resident) {  // full-sweep mode
         const int64_t rem_tiles = p.n_utiles % resident;
         // measured: a 67-tile tail (of 256) runs faster as a split launch, a 135-tile one slower
@@ -1798,8 +1875,9 @@ extern "C" int lgx_score_topk_workspace(int64_t B, int64_t n_items, int k, size_
     LGX_REQUIRE(ws_bytes && B >= 0 && n_items >= 0 && k >= 1, LGX_ERR_INVALID_ARG,
                 "lgx_score_topk_workspace: bad arguments");
     // the split plan depends on dtype / d; report the maximum over every kernel variant
-    size_t m = topk_ws_bytes(B, n_items, k, LGX_DTYPE_F32, 64);
-    for (int64_t d = 32; d <= 256; d += 16) m = std::max(m, topk_ws_bytes(B, n_items, k, LGX_DTYPE_BF16, d));
+    size_t m = 0;
+    for (int64_t d = 16; d <= 256; d += 16)
+        m = std::max({m, topk_ws_bytes(B, n_items, k, LGX_DTYPE_BF16, d), topk_ws_bytes(B, n_items, k, LGX_DTYPE_F32, d)});
     *ws_bytes = m;
     return LGX_OK;
 }
@@ -1813,7 +1891,8 @@ extern "C" int lgx_score_topk_plan(int64_t B, int64_t n_items, int64_t d, int dt
     size_t off = 0;
     for (int i = 0; i < n && off < len; ++i) {
         const SplitPlan& p = r[i].p;
-        const char* kern = p.lds ? "score_topk_bf16_lds<8 waves, 64-item tiles, 16x16x32>"
+        const char* kern = p.lds ? (dtype == LGX_DTYPE_F32 ? "score_topk_f32_lds<4 waves, 64-item tiles, 16x16x4>"
+                                                           : "score_topk_bf16_lds<8 waves, 64-item tiles, 16x16x32>")
                                  : (v1_waves(k) == 4 ? "score_topk_kernel<4 waves>" : "score_topk_kernel<1 wave>");
         const char* mode = p.lds ? (p.n_splits == 1 ? "full-sweep" : (p.xcd_affine ? "split-xcd" : "split"))
                                  : "split";
@@ -1895,10 +1974,10 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
                     st.seed_score = a.part_score;
                     st.seed_idx = a.part_idx;
                 }
-                rc = launch_lds<false>(st, p, stream);
+                rc = launch_lds<false>(st, p, stream, dtype);
                 if (st.n_items == n_items) break;
             }
-        } else if (p.lds) rc = mm ? launch_lds<true>(a, p, stream) : launch_lds<false>(a, p, stream);
+        } else if (p.lds) rc = mm ? launch_lds<true>(a, p, stream, dtype) : launch_lds<false>(a, p, stream, dtype);
         else if (dtype == LGX_DTYPE_F32) rc = mm ? launch_v1<LGX_DTYPE_F32, true>(a, kch, stream)
                                                  : launch_v1<LGX_DTYPE_F32, false>(a, kch, stream);
         else rc = mm ? launch_v1<LGX_DTYPE_BF16, true>(a, kch, stream)

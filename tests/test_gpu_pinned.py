@@ -321,11 +321,11 @@ def test_c5_full_catalog_1m_items_bench_plan():
 
 def test_c5_fp32_scoring_leg_plan_and_values():
     """The fp32 scoring leg of the bench (the reference's precision, model.py:183): f32 query and
-    item tables through score_topk_kernel<f32>, 16,384 users x 1,000,000 items, d=256, masked,
+    item tables through score_topk_f32_lds (16x16x4 f32 MFMA), 16,384 users x 1,000,000 items, d=256, masked,
     checked against float64 for 1,000 users."""
     B, I, d, k = 16384, 1_000_000, 256, 20
     plan = ops.score_topk_plan(B, I, d, torch.float32, k)
-    assert all(p.startswith("score_topk_kernel") for p in plan.split("; ")), plan
+    assert all(p.startswith("score_topk_f32_lds") for p in plan.split("; ")), plan
     g = torch.Generator(device=DEV).manual_seed(57)
     Q = torch.randn(B, d, device=DEV, generator=g) / 16
     items = torch.randn(I, d, device=DEV, generator=g) / 16

@@ -1,0 +1,129 @@
+"""GPU: the fp32 scoring path (the reference's precision: model.py:183 fp32 matmul + Procedure.py:
+134-135 mask and torch.topk) through score_topk_f32_lds -- the LDS-ring walk on
+v_mfma_f32_16x16x4_f32 -- in every launch mode the planner uses: catalog split (small batches),
+full sweep (>= 256 user tiles of 128), full sweep seeded in stages (>= 262 144 items), the split tail
+of a partial last round, user_rows, the min / max variant; and the fall-back kernel where the LDS
+budget rules the walk out (d = 256 with k > 20).  Checked on the device against float64 scores:
+k distinct unmasked items, each within 1e-5 of the exact k-th best, values = the float64 scores to
+1e-5 (fp32 products and sums of |x| ~ 1 inputs over d <= 256)."""
+import numpy as np
+import pytest
+import torch
+
+import factors_of_serendipity_recommendation_amd as lgx
+from factors_of_serendipity_recommendation_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _mask(B, I, per, g):
+    m = torch.randint(0, I, (B, per), device=DEV, generator=g).sort(1).values
+    keep = torch.ones_like(m, dtype=torch.bool)
+    keep[:, 1:] = m[:, 1:] != m[:, :-1]
+    indptr = torch.zeros(B + 1, dtype=torch.int64, device=DEV)
+    indptr[1:] = torch.cumsum(keep.sum(1), 0)
+    return indptr, m[keep].to(torch.int32)
+
+
+def _check(Q, items, idx, val, mask, sel, k, user_rows=None, chunk=250):
+    items64 = items.double()
+    for c0 in range(0, sel.numel(), chunk):
+        s = sel[c0:c0 + chunk]
+        qs = user_rows[s] if user_rows is not None else s
+        S = Q[qs].double() @ items64.T
+        if mask is not None:
+            indptr, mi = mask
+            for j, u in enumerate(s.tolist()):
+                S[j, mi[indptr[u]:indptr[u + 1]].long()] = float("-inf")
+        kth = torch.topk(S, k, dim=1).values[:, -1:]
+        got_idx = idx[s].long()
+        assert (got_idx >= 0).all()
+        got = S.gather(1, got_idx)
+        assert torch.isfinite(got).all(), "a masked item was returned"
+        assert (got >= kth - 1e-5 * kth.abs().clamp(min=1.0)).all()
+        srt = got_idx.sort(1).values
+        assert (srt[:, 1:] != srt[:, :-1]).all()
+        assert torch.allclose(val[s].double(), got, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("d,k,lds", [(64, 20, True), (128, 32, True), (192, 7, True), (256, 20, True),
+                                     (256, 21, False), (96, 20, False), (32, 20, False)])
+def test_f32_kernel_selection(d, k, lds):
+    plan = ops.score_topk_plan(40_000, 100_000, d, torch.float32, k)
+    assert plan.startswith("score_topk_f32_lds") == lds, plan
+
+
+@pytest.mark.parametrize("B,I,d,k,per", [(1000, 50_000, 64, 20, 30), (3000, 20_011, 256, 20, 50),
+                                         (777, 40_000, 128, 32, 10), (5000, 30_000, 192, 1, 40)])
+def test_f32_split_mode(B, I, d, k, per):
+    plan = ops.score_topk_plan(B, I, d, torch.float32, k)
+    assert plan.startswith("score_topk_f32_lds") and "split" in plan, plan
+    g = torch.Generator(device=DEV).manual_seed(B + d)
+    Q = torch.randn(B, d, device=DEV, generator=g) / 8
+    items = torch.randn(I, d, device=DEV, generator=g) / 8
+    mask = _mask(B, I, per, g)
+    idx, val = lgx.score_topk(Q, items, k, mask=mask)
+    _check(Q, items, idx, val, mask, torch.arange(0, B, max(1, B // 600), device=DEV), k)
+
+
+def test_f32_full_sweep_with_split_tail_and_user_rows():
+    """256 full user tiles of 128 plus a 40-tile partial round (its own split launch), user_rows
+    permuting a larger query table, masked."""
+    B, I, d, k = 128 * (256 + 40), 30_000, 256, 20
+    plan = ops.score_topk_plan(B, I, d, torch.float32, k)
+    assert "full-sweep" in plan and plan.count("score_topk_f32_lds") == 2, plan
+    g = torch.Generator(device=DEV).manual_seed(3)
+    Q = torch.randn(B + 500, d, device=DEV, generator=g) / 8
+    items = torch.randn(I, d, device=DEV, generator=g) / 8
+    rows = torch.randperm(B + 500, device=DEV, generator=g)[:B]
+    mask = _mask(B, I, 50, g)
+    idx, val = lgx.score_topk(Q, items, k, user_rows=rows, mask=mask)
+    sel = torch.cat([torch.randint(0, 128 * 256, (600,), device=DEV, generator=g),
+                     torch.randint(128 * 256, B, (600,), device=DEV, generator=g)])
+    _check(Q, items, idx, val, mask, sel, k, user_rows=rows)
+
+
+def test_f32_seeded_stages_equal_one_sweep_and_float64():
+    """>= 262 144 items: the sweep runs in seeded stages; the lists equal (as sets) the unseeded
+    one-launch min / max variant and the float64 top-k; min / max equal the float64 extremes."""
+    B, I, d, k = 128 * 256, 300_000, 128, 20
+    plan = ops.score_topk_plan(B, I, d, torch.float32, k)
+    assert "full-sweep (seeded in stages)" in plan and plan.startswith("score_topk_f32_lds"), plan
+    g = torch.Generator(device=DEV).manual_seed(5)
+    Q = torch.randn(B, d, device=DEV, generator=g) / 8
+    items = torch.randn(I, d, device=DEV, generator=g) / 8
+    mask = _mask(B, I, 40, g)
+    idx, val = lgx.score_topk(Q, items, k, mask=mask)
+    idx1, val1, mm = lgx.score_topk(Q, items, k, mask=mask, want_minmax=True)
+    ka, kb = torch.sort(idx.long(), 1), torch.sort(idx1.long(), 1)
+    assert torch.equal(ka.values, kb.values), "seeded lists differ from the one-launch sweep"
+    assert torch.equal(val.gather(1, ka.indices), val1.gather(1, kb.indices))
+    _check(Q, items, idx, val, mask, torch.randint(0, B, (1000,), device=DEV, generator=g), k)
+    lo, hi = float("inf"), float("-inf")
+    for u0 in range(0, B, 2048):
+        S = Q[u0:u0 + 2048].double() @ items.double().T
+        lo, hi = min(lo, S.min().item()), max(hi, S.max().item())
+    m = mm.cpu().numpy().astype(np.float64)
+    assert abs(m[0] - lo) <= 1e-5 * abs(lo) + 1e-6 and abs(m[1] - hi) <= 1e-5 * abs(hi) + 1e-6, (m, lo, hi)
+
+
+def test_f32_sigmoid_and_mask_value_like_procedure_test():
+    """Procedure.Test's call: sigmoid scores, positives at -(1 << 10); a user with every item but
+    3 masked gets those 3 then the masked tail (mask_value, the masked items in order)."""
+    B, I, d, k = 300, 5000, 64, 20
+    g = torch.Generator(device=DEV).manual_seed(8)
+    Q = torch.randn(B, d, device=DEV, generator=g) / 8
+    items = torch.randn(I, d, device=DEV, generator=g) / 8
+    lists = [sorted(set(torch.randint(0, I, (30,), generator=torch.Generator().manual_seed(u)).tolist()))
+             for u in range(B)]
+    lists[7] = [i for i in range(I) if i not in (5, 77, 4000)]
+    mask = ops.lists_to_device_csr(lists, DEV)
+    idx, val = lgx.score_topk(Q, items, k, mask=mask, mask_value=-float(1 << 10), apply_sigmoid=True)
+    assert sorted(idx[7, :3].tolist()) == [5, 77, 4000]
+    assert (val[7, 3:] == -1024.0).all() and idx[7, 3:].tolist() == lists[7][:k - 3]
+    S = torch.sigmoid((Q.double() @ items.double().T))
+    for u in (0, 1, 100, 299):
+        S[u, torch.tensor(lists[u], device=DEV)] = -1.0
+        want = torch.topk(S[u], k).values
+        assert torch.allclose(val[u].double(), want, rtol=1e-6, atol=1e-6)
