@@ -87,6 +87,8 @@ SIGNATURES = {
     "lgx_propagate": (_c_int, [ctypes.POINTER(LgxCSR), _vp, _vp, _c_i64, _c_int, _c_int, _vp, ctypes.c_size_t, _vp]),
     "lgx_score_dense": (_c_int, [_vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _vp, _vp]),
     "lgx_score_topk_workspace": (_c_int, [_c_i64, _c_i64, _c_int, _sz_p]),
+    "lgx_score_minmax_workspace": (_c_int, [_c_i64, _c_i64, _sz_p]),
+    "lgx_score_minmax": (_c_int, [_vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _vp, _vp, ctypes.c_size_t, _vp]),
     "lgx_score_topk": (_c_int, [_vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _vp, _vp, _c_int, ctypes.c_float,
                                 _c_int, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "lgx_topk_rows": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _c_int, _vp, _vp, _vp]),

@@ -738,6 +738,11 @@ __global__ __launch_bounds__(WPB * 64) void score_topk_kernel(ScoreArgs a) {
 // Workgroup shape: WAVES x 32 users, tiles of 32*NACC items.  <8, 2> (one 512-thread workgroup per
 // CU, 64-item tiles) is the one launched; see lds_waves() for the measured alternative.
 
+// ABLATE value of the LDS walk that keeps only the global min / max of the scores (no top-k state
+// touched): lgx_score_minmax, the reference's np.max / np.min over the full U x I matrix
+// (recommend.py:163-164, :377).  A product mode, not a development ablation.
+constexpr int kMinMaxOnly = 10;
+
 template <int KSTEPS, int WAVES = 8, int NACC = 2, int ESZ = 2>
 struct LdsGeom {
     static constexpr int TILE_ITEMS = 32 * NACC;
@@ -1027,7 +1032,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
                     if (s2 + 1 < KS2) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 }
             }
-            if (!SKIP) regroup();
+            if (!SKIP && ABLATE != kMinMaxOnly) regroup();
         } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -1064,7 +1069,29 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         }
     };
     // the split's last tile is the only one that can run past i_end: a block variant of its own
+    // min / max mode: every score of the tile straight from the MFMA layout.  Rows past the split's
+    // end re-read its last item (stage_piece), so they hold real scores; padding users do not.
+    const bool uok0 = utile * G::USERS + wave * kUsersPerWave + r16 < a.B;
+    const bool uok1 = utile * G::USERS + wave * kUsersPerWave + 16 + r16 < a.B;
+    auto minmax_tile = [&]() {
+        float lo0 = c[0][0][0], hi0 = c[0][0][0], lo1 = c[1][0][0], hi1 = c[1][0][0];
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                lo0 = fminf(lo0, c[0][ib][r]);
+                hi0 = fmaxf(hi0, c[0][ib][r]);
+                lo1 = fminf(lo1, c[1][ib][r]);
+                hi1 = fmaxf(hi1, c[1][ib][r]);
+            }
+        st.mn = fminf(st.mn, fminf(uok0 ? lo0 : INFINITY, uok1 ? lo1 : INFINITY));
+        st.mx = fmaxf(st.mx, fmaxf(uok0 ? hi0 : -INFINITY, uok1 ? hi1 : -INFINITY));
+    };
     auto epilogue = [&](int64_t e0) {
+        if constexpr (ABLATE == kMinMaxOnly) {
+            minmax_tile();
+            return;
+        }
         const bool tail = e0 + G::TILE_ITEMS > i_end;
         if constexpr (SKIP) {
             if (!tail) {
@@ -1179,6 +1206,18 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         sbuf = sbuf + 1 == nbuf ? 0 : sbuf + 1;
     }
     if (late && ntiles > 0) epilogue(prev_t0);
+    if constexpr (ABLATE == kMinMaxOnly) {
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) {
+            st.mn = fminf(st.mn, __shfl_xor(st.mn, m, 64));
+            st.mx = fmaxf(st.mx, __shfl_xor(st.mx, m, 64));
+        }
+        if (lane == 0 && st.mn <= st.mx) {
+            atomicMin(a.minmax, ord_f32(st.mn));
+            atomicMax(a.minmax + 1, ord_f32(st.mx));
+        }
+        return;
+    }
     st.flush(a, split, lane);
 #ifdef LGX_SCORE_STATS
     { uint64_t* stat_ = st.stat_; LGX_STAT_FLUSH }
@@ -1195,12 +1234,17 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
 }
 
 constexpr int kF32LdsWaves = 4;
-template <int KSTEPS, bool MINMAX>
+template <int KSTEPS, bool MINMAX, int MODE = 0>
 __global__ __launch_bounds__(kF32LdsWaves * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void score_topk_f32_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    score_topk_lds_body<LGX_DTYPE_F32, KSTEPS, MINMAX, 0, kF32LdsWaves, 2, false, true, 0, true>(
+    score_topk_lds_body<LGX_DTYPE_F32, KSTEPS, MINMAX, MODE, kF32LdsWaves, 2, false, true, 0, true>(
         smem, a, xcd_affine, n_utiles, nbuf);
+}
+
+__global__ void minmax_finish(const uint32_t* mm, float* out) {
+    out[0] = unord_f32(mm[0]);
+    out[1] = unord_f32(mm[1]);
 }
 
 // one wave per query: merge the split lists, masked tail, optional sigmoid (k <= 64 R)
@@ -1751,7 +1795,7 @@ int launch_lds_shape(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream)
     return launch_lds_kernel<KS, MM, ABL, WAVES, NACC, true, true>(a, p, stream);
 }
 
-template <int KS, bool MM>
+template <int KS, bool MM, int MODE = 0>
 int launch_f32_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     typedef LdsGeom<KS, kF32LdsWaves, 2, 4> G;
     const size_t lists = (size_t)kF32LdsWaves * list_bytes_per_wave(a.k);
@@ -1761,10 +1805,11 @@ int launch_f32_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t st
         set_error("lgx_score_topk: f32 LDS kernel needs %zu B of LDS", shmem);
         return LGX_ERR_UNSUPPORTED;
     }
-    int rc = set_lds_limit(score_topk_f32_lds<KS, MM>, shmem);
+    int rc = set_lds_limit(score_topk_f32_lds<KS, MM, MODE>, shmem);
     if (rc) return rc;
     const unsigned grid = (unsigned)(p.n_utiles * p.n_splits);
-    score_topk_f32_lds<KS, MM><<<grid, kF32LdsWaves * 64, shmem, stream>>>(a, p.xcd_affine ? 1 : 0, p.n_utiles, nbuf);
+    score_topk_f32_lds<KS, MM, MODE><<<grid, kF32LdsWaves * 64, shmem, stream>>>(a, p.xcd_affine ? 1 : 0,
+                                                                                   p.n_utiles, nbuf);
     LGX_LAUNCH_CHECK();
     return LGX_OK;
 }
@@ -1772,20 +1817,20 @@ int launch_f32_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t st
 template <bool MM, int ABL = 0>
 int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream, int dtype = LGX_DTYPE_BF16) {
     const int ksteps = (int)(a.d / 16);
-    if constexpr (ABL == 0) {
+    if constexpr (ABL == 0 || ABL == kMinMaxOnly) {
         if (dtype == LGX_DTYPE_F32) {
             switch (ksteps) {
-                case 4: return launch_f32_lds_kernel<4, MM>(a, p, stream);
-                case 8: return launch_f32_lds_kernel<8, MM>(a, p, stream);
-                case 12: return launch_f32_lds_kernel<12, MM>(a, p, stream);
-                case 16: return launch_f32_lds_kernel<16, MM>(a, p, stream);
+                case 4: return launch_f32_lds_kernel<4, MM, ABL>(a, p, stream);
+                case 8: return launch_f32_lds_kernel<8, MM, ABL>(a, p, stream);
+                case 12: return launch_f32_lds_kernel<12, MM, ABL>(a, p, stream);
+                case 16: return launch_f32_lds_kernel<16, MM, ABL>(a, p, stream);
                 default:
                     set_error("lgx_score_topk: no f32 LDS kernel for d=%lld", (long long)a.d);
                     return LGX_ERR_UNSUPPORTED;
             }
         }
     }
-    if constexpr (ABL != 0) {  // development ablations: d = 256 only
+    if constexpr (ABL != 0 && ABL != kMinMaxOnly) {  // development ablations: d = 256 only
         if (ksteps != 16) {
             set_error("lgx_score_topk: ablation builds exist for d=256 only");
             return LGX_ERR_UNSUPPORTED;
@@ -1992,6 +2037,54 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
         else score_topk_finalize<4><<<(unsigned)Bi, 64, 0, stream>>>(a, mask_value, apply_sigmoid, oi, ov, om);
         LGX_LAUNCH_CHECK();
     }
+    return LGX_OK;
+}
+
+extern "C" int lgx_score_minmax_workspace(int64_t B, int64_t n_items, size_t* ws_bytes) {
+    LGX_REQUIRE(ws_bytes && B >= 0 && n_items >= 0, LGX_ERR_INVALID_ARG, "lgx_score_minmax_workspace: bad arguments");
+    size_t topk = 0;
+    const int rc = lgx_score_topk_workspace(B, n_items, 1, &topk);
+    if (rc) return rc;
+    // the LDS walk needs the 2 ordered words only; shapes it does not cover go through the top-1
+    // path, which needs its workspace plus [B] index / value outputs
+    *ws_bytes = 512 + align_up(topk) + 2 * align_up((size_t)B * 4);
+    return LGX_OK;
+}
+
+extern "C" int lgx_score_minmax(const void* Q, const int64_t* user_rows, const void* items, int64_t B, int64_t n_items,
+                                int64_t d, int dtype, float* minmax_out, void* ws, size_t ws_bytes,
+                                lgx_stream_t stream_) {
+    hipStream_t stream = as_hip(stream_);
+    LGX_REQUIRE(B > 0 && n_items > 0 && n_items < INT32_MAX && Q && items && minmax_out, LGX_ERR_INVALID_ARG,
+                "lgx_score_minmax: bad arguments");
+    LGX_REQUIRE(dtype == LGX_DTYPE_F32 || dtype == LGX_DTYPE_BF16, LGX_ERR_INVALID_ARG, "lgx_score_minmax: dtype");
+    const int64_t vec = dtype == LGX_DTYPE_F32 ? 4 : 8;
+    LGX_REQUIRE(d > 0 && d % vec == 0 && kch_for(dtype, d) > 0, LGX_ERR_UNSUPPORTED,
+                "lgx_score_minmax: d=%lld must be a multiple of %lld and <= 256", (long long)d, (long long)vec);
+    size_t need = 0;
+    lgx_score_minmax_workspace(B, n_items, &need);
+    LGX_REQUIRE(ws && ws_bytes >= need, LGX_ERR_WORKSPACE, "lgx_score_minmax: workspace %zu < %zu", ws_bytes, need);
+    char* base = static_cast<char*>(ws);
+    uint32_t* mm = reinterpret_cast<uint32_t*>(base);
+    const bool lds_ok = lds_eligible(dtype, d, 1) &&
+                        (dtype == LGX_DTYPE_BF16 ? (d / 16) % 2 == 0 : (d / 16) % 4 == 0);
+    if (!lds_ok) {  // the top-1 launch with its min / max output
+        size_t topk = 0;
+        lgx_score_topk_workspace(B, n_items, 1, &topk);
+        int32_t* oi = reinterpret_cast<int32_t*>(base + 512 + align_up(topk));
+        float* ov = reinterpret_cast<float*>(base + 512 + align_up(topk) + align_up((size_t)B * 4));
+        return lgx_score_topk(Q, user_rows, items, B, n_items, d, dtype, nullptr, nullptr, 1, -INFINITY, 0, oi, ov,
+                              minmax_out, base + 512, align_up(topk), stream_);
+    }
+    minmax_init<<<1, 1, 0, stream>>>(mm);
+    LGX_LAUNCH_CHECK();
+    const SplitPlan p = plan_splits(B, n_items, dtype, d, 1);
+    ScoreArgs a{Q, user_rows, items, B, n_items, d, nullptr, nullptr, 1, p.n_splits, p.split_items,
+                nullptr, nullptr, mm, nullptr};
+    const int rc = launch_lds<false, kMinMaxOnly>(a, p, stream, dtype);
+    if (rc) return rc;
+    minmax_finish<<<1, 1, 0, stream>>>(mm, minmax_out);
+    LGX_LAUNCH_CHECK();
     return LGX_OK;
 }
 

@@ -276,15 +276,17 @@ __global__ __launch_bounds__(kStratThreads) void strat_select_kernel(const int8_
     }
     __syncthreads();
     // Fast path: the keys are uniform 64-bit hashes, so the need[l] smallest of label l lie below
-    // cut[l] = 2^64 (need[l] + 4 sqrt(need[l]) + 8) / hist[l] but for a ~4-sigma shortfall.  One pass
-    // gathers every key under its label's cut into LDS (expected K + a few hundred), and the exact
-    // need[l] smallest per label are ranked there: the same picks as the radix select below, which
-    // runs only when a label came up short or the buffer overflowed.
+    // cut[l] = 2^64 (need[l] + 6 sqrt(need[l]) + 16) / hist[l] but for a ~5.7-sigma shortfall (a
+    // 4-sigma margin failed for ~1 user per 4096-user batch, and that user's 8-pass radix select
+    // stretched the launch 2.3 -> 11 ms).  One pass gathers every key under its label's cut into LDS
+    // (expected K + 6 sum sqrt(need) + 16 n_bins, ~1840 at K = 1024 over 11 labels, under the 2048
+    // slots), and the exact need[l] smallest per label are ranked there: the same picks as the radix
+    // select below, which runs only when a label came up short or the buffer overflowed.
     uint64_t* ck = reinterpret_cast<uint64_t*>(dh);
     int32_t* ci = reinterpret_cast<int32_t*>(ck + kMaxCand);
     if (tid < n_bins) {
         const int64_t hl = hist[u * n_bins + tid], nl = need[tid];
-        const double frac = hl > 0 ? ((double)nl + 4.0 * sqrt((double)nl) + 8.0) / (double)hl : 2.0;
+        const double frac = hl > 0 ? ((double)nl + 6.0 * sqrt((double)nl) + 16.0) / (double)hl : 2.0;
         cut[tid] = nl <= 0 ? 0ull : (frac >= 1.0 ? ~0ull : (uint64_t)(frac * 18446744073709551616.0));
         cand_l[tid] = 0;
     }

@@ -244,6 +244,29 @@ def score_topk(Q: torch.Tensor, items: torch.Tensor, k: int, user_rows: Optional
     return (idx, val, mm) if want_minmax else (idx, val)
 
 
+def score_minmax(Q: torch.Tensor, items: torch.Tensor, user_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Global (min, max) of Q . items^T over every pair (``lgx_score_minmax``) -> f32 [2] on the
+    device (recommend.py:163-164, :375-377)."""
+    require_gpu(Q, items, user_rows)
+    check_pair(Q, items)
+    Q = Q.contiguous()
+    items = items.contiguous()
+    B = user_rows.numel() if user_rows is not None else Q.shape[0]
+    if B == 0 or items.shape[0] == 0:
+        raise ValueError("score_minmax of an empty matrix")
+    rows = user_rows.to(torch.int64).contiguous() if user_rows is not None else None
+    dev = Q.device
+    L = _lib.lib()
+    ws = ctypes.c_size_t(0)
+    _lib.check(L.lgx_score_minmax_workspace(B, items.shape[0], ctypes.byref(ws)), "lgx_score_minmax_workspace")
+    work = torch.empty(max(ws.value, 1), dtype=torch.uint8, device=dev)
+    mm = torch.empty(2, dtype=torch.float32, device=dev)
+    _lib.check(L.lgx_score_minmax(Q.data_ptr(), _ptr(rows), items.data_ptr(), B, items.shape[0], Q.shape[1],
+                                  _dtype_code(Q), mm.data_ptr(), work.data_ptr(), ws.value, _stream_ptr(dev)),
+               "lgx_score_minmax")
+    return mm
+
+
 def topk_rows(S: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
     """Row-wise top-k of a dense f32 score matrix (tools.h:13-33); ties -> lower column."""
     require_gpu(S)

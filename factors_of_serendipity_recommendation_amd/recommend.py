@@ -81,8 +81,7 @@ def accuracy_cf(mat_candidate: Dict[int, List[int]], dataset_name: str, seed: in
 
 def similarity_minmax(emb_user: torch.Tensor, emb_item: torch.Tensor) -> Tuple[float, float]:
     """(min, max) of emb_user . emb_item^T over all pairs (recommend.py:163-164)."""
-    _, _, mm = ops.score_topk(emb_user.contiguous(), emb_item.contiguous(), 1, want_minmax=True)
-    mm = mm.cpu().numpy()
+    mm = ops.score_minmax(emb_user, emb_item).cpu().numpy()
     return float(mm[0]), float(mm[1])
 
 

@@ -189,7 +189,8 @@ int lgx_score_topk_workspace(int64_t B, int64_t n_items, int k, size_t* ws_bytes
  *   (may be NULL).  Masked items rank after every unmasked item with value mask_value.
  *   Ranking: higher raw score first, ties -> lower item id.  out_val = raw score, or
  *   sigmoid(score) if apply_sigmoid.  minmax_out (NULL = skip) receives {min, max} of ALL raw
- *   scores (before masking) as f32[2].  k in [1, 256] (k <= 32 runs the LDS-staged bf16 kernel).
+ *   scores (before masking) as f32[2].  k in [1, 256]; k <= 32 (bf16, d a multiple of 32) and
+ *   k <= 20 (f32, d a multiple of 64; larger k where the LDS budget allows) run the LDS-staged walk.
  *   Full sweeps over >= 262144 items (and no minmax_out) run as several stream-ordered launches
  *   over consecutive item ranges, each seeding the next through the workspace's lists.
  */
@@ -203,6 +204,15 @@ int lgx_score_topk(const void* Q, const int64_t* user_rows, const void* items, i
  * kernel, user ranges, full-sweep / catalog-split mode -- as text.  No device work.
  */
 int lgx_score_topk_plan(int64_t B, int64_t n_items, int64_t d, int dtype, int k, char* buf, size_t len);
+/*
+ * Global {min, max} of the raw scores <Q[b], items[i]> over ALL (b, i) -> minmax_out f32[2]: the
+ * reference's np.max / np.min of the full user x item dot matrix (recommend.py:163-164, :375-377).
+ * The LDS scoring walk with nothing but a running min / max per lane (no top-k state); shapes that
+ * walk does not cover go through the top-1 launch of lgx_score_topk.  Needs the workspace below.
+ */
+int lgx_score_minmax_workspace(int64_t B, int64_t n_items, size_t* ws_bytes);
+int lgx_score_minmax(const void* Q, const int64_t* user_rows, const void* items, int64_t B, int64_t n_items,
+                     int64_t d, int dtype, float* minmax_out, void* ws, size_t ws_bytes, lgx_stream_t stream);
 /* Row-wise top-k of a dense f32 matrix (row stride ld), ties -> lower column.  k in [1, 256]. */
 int lgx_topk_rows(const float* S, int64_t rows, int64_t cols, int64_t ld, int k, int32_t* out_idx,
                   float* out_val, lgx_stream_t stream);

@@ -127,3 +127,26 @@ def test_f32_sigmoid_and_mask_value_like_procedure_test():
         S[u, torch.tensor(lists[u], device=DEV)] = -1.0
         want = torch.topk(S[u], k).values
         assert torch.allclose(val[u].double(), want, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("dtype,B,I,d,rows", [(torch.float32, 16384, 100_003, 64, False),
+                                              (torch.float32, 333, 50_000, 256, True),
+                                              (torch.float32, 1000, 20_000, 96, False),     # top-1 fall-back
+                                              (torch.bfloat16, 40_000, 70_001, 128, False),
+                                              (torch.bfloat16, 77, 5_000, 256, True)])
+def test_score_minmax_vs_float64(dtype, B, I, d, rows):
+    """lgx_score_minmax (np.max / np.min of the full dot matrix, recommend.py:163-164, :377): the
+    LDS walk's min / max mode (f32 and bf16, full-sweep and split plans, padding users, a ragged
+    last tile, user_rows) and the top-1 fall-back, against float64 on the device."""
+    g = torch.Generator(device=DEV).manual_seed(B + d)
+    n_q = B + 100 if rows else B
+    Q = (torch.randn(n_q, d, device=DEV, generator=g) / 8).to(dtype)
+    items = (torch.randn(I, d, device=DEV, generator=g) / 8).to(dtype)
+    user_rows = torch.randperm(n_q, device=DEV, generator=g)[:B] if rows else None
+    mm = ops.score_minmax(Q, items, user_rows=user_rows).cpu().numpy().astype(np.float64)
+    Qs = Q[user_rows] if rows else Q
+    lo, hi = float("inf"), float("-inf")
+    for u0 in range(0, B, 2048):
+        S = Qs[u0:u0 + 2048].double() @ items.double().T
+        lo, hi = min(lo, S.min().item()), max(hi, S.max().item())
+    assert abs(mm[0] - lo) <= 1e-5 * abs(lo) + 1e-6 and abs(mm[1] - hi) <= 1e-5 * abs(hi) + 1e-6, (mm, lo, hi)

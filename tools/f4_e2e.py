@@ -66,3 +66,35 @@ print(f"f4 end-to-end, {U} users x {I} items: synchronous per-batch lists {ms_sy
       f"stratified_candidates (lazy CandidateLists) {ms_pipe:.1f} ms from Python train lists, {ms_csr:.1f} ms "
       f"from a device CSR ({U / ms_csr * 1e3:.0f} users/s); materialising every row as a list afterwards "
       f"{ms_rows:.1f} ms; lists identical", flush=True)
+
+# component times (HIP events on the current stream): bounds pass, fused labels + counts, select
+from factors_of_serendipity_recommendation_amd import _lib  # noqa: E402
+
+
+def ev_time(fn, reps=3):
+    fn()
+    out = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        out.append(a.elapsed_time(b))
+    return float(np.median(out))
+
+
+min16, inter16 = recommend.stratification_bounds(Eu, Ei, 10, 0.1)
+mp, mi = csr
+t_b = ev_time(lambda: recommend.stratification_bounds(Eu, Ei, 10, 0.1))
+t_l = ev_time(lambda: recommend.strat_labels(Eu[:B], Ei, mp, mi, min16, inter16, 10, None))
+lab, hist = recommend.strat_labels(Eu[:B], Ei, mp, mi, min16, inter16, 10, None)
+o = torch.empty((B, 1000), dtype=torch.int32, device="cuda")
+cn = torch.empty(B, dtype=torch.int32, device="cuda")
+tg = torch.full((B,), 1000, dtype=torch.int32, device="cuda")
+L = _lib.lib()
+t_s = ev_time(lambda: _lib.check(L.lgx_strat_select(lab.data_ptr(), B, I, hist.data_ptr(), 11, tg.data_ptr(), 7,
+                                                    o.data_ptr(), 1000, cn.data_ptr(),
+                                                    ops._stream_ptr(torch.device("cuda"))), "select"))
+print(f"f4 components per {B}-user batch: bounds pass (all {U} users) {t_b:.2f} ms, fused labels + counts "
+      f"{t_l:.2f} ms, select {t_s:.2f} ms", flush=True)
