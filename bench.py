@@ -155,8 +155,12 @@ def layer_models(A, d: int, s: int, mode: int, n_prev: int = 0, shard_op: bool =
     epi = epilogue_bytes(mode, rows, d, s, n_prev)
     cold, R, hot_frac = cold_gather_cols(A, d, s) if shard_op else cold_gather_rows(A, d, s)
     floor = nnz * 8 + (rows + N) * d * s if shard_op else nnz * 8 + 2 * N * d * s
-    return {"model": csr + epi + cold * d * s, "gathered": csr + epi + nnz * d * s,
-            "floor": floor, "hot_rows": R, "hot_frac": hot_frac,
+    # column-blocked item rows: the f32 row sums carried between the nb block launches (written by
+    # blocks 0..nb-2, read by blocks 1..nb-1) plus the nb-1 extra block pointers per item row
+    nb = A.col_block_count(d, s)
+    carry = (2 * (nb - 1) * A.n_items * d * 4 + 8 * (nb - 1) * A.n_items) if nb > 1 else 0
+    return {"model": csr + epi + carry + cold * d * s, "gathered": csr + epi + carry + nnz * d * s,
+            "floor": floor, "hot_rows": R, "hot_frac": hot_frac, "col_blocks": nb,
             "kernel": ops.spmm_kernel_name(d, torch.bfloat16 if s == 2 else torch.float32, A.plan.seg_len)}
 
 
@@ -269,11 +273,16 @@ def bench_propagation(args, rank, world, A, cfg, dtype, steps, warmup):
     hot_rows = timings[0][2]["hot_rows"]
     hot_frac = float(np.mean([m["hot_frac"] for _, _, m in timings]))
     kernels = sorted({m["kernel"] for _, _, m in timings})
-    traffic, tsrc = measured_traffic(cfg.name, dname, world, ["spmm_segments", "spmm_fixup"])
+    col_blocks = max(m.get("col_blocks", 0) for _, _, m in timings)
+    # per layer call: with column blocks one call is 1 + nb dispatches of spmm_segments
+    traffic, tsrc = measured_traffic(cfg.name, dname, world, ["spmm_segments", "spmm_fixup"],
+                                     calls_from=("spmm_segments", 1 + col_blocks) if col_blocks > 1 else None)
     achieved = mean["model"] / mean_launch_s
     roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": achieved / HBM_PEAK, "traffic": traffic,
-            "kernel": "spmm_segments (+spmm_fixup): " + ", ".join(kernels),
+            "kernel": "spmm_segments (+spmm_fixup): " + ", ".join(kernels)
+                      + (f"; item rows in {col_blocks} column blocks (1 + {col_blocks} launches per layer)"
+                         if col_blocks > 1 else ""),
             "mean_launch_ms": mean_launch_s * 1e3,
             "bytes_model": "cache-aware: CSR + epilogue + gathers of rows outside the per-XCD L2 hot set "
                            f"(top {hot_rows} rows per gathered table = {hot_frac:.3f} of gathers)"

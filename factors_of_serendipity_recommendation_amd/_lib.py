@@ -31,6 +31,17 @@ _vp = ctypes.c_void_p
 _sz_p = ctypes.POINTER(ctypes.c_size_t)
 
 
+class LgxPlan(ctypes.Structure):
+    """Mirror of ``struct lgx_plan`` (include/lgx.h)."""
+
+    _fields_ = [
+        ("seg_row", _vp), ("seg_part", _vp), ("seg_slot", _vp),
+        ("n_segs", _c_i64), ("seg_len", _c_i64),
+        ("split_row", _vp), ("split_ptr", _vp),
+        ("n_split", _c_i64), ("n_partials", _c_i64), ("partials", _vp),
+    ]
+
+
 class LgxCSR(ctypes.Structure):
     """Mirror of ``struct lgx_csr`` (include/lgx.h)."""
 
@@ -41,6 +52,8 @@ class LgxCSR(ctypes.Structure):
         ("n_segs", _c_i64), ("seg_len", _c_i64),
         ("split_row", _vp), ("split_ptr", _vp),
         ("n_split", _c_i64), ("n_partials", _c_i64), ("partials", _vp),
+        ("cb_row0", _c_i64), ("cb_n", _c_i64), ("cb_ptr", _vp),
+        ("cb_plans", ctypes.POINTER(LgxPlan)), ("cb_carry", _vp),
     ]
 
 

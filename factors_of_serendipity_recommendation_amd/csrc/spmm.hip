@@ -19,7 +19,10 @@
 //   * the epilogue writes the next layer table AND folds the layer into the fp32 running sum, and
 //     the last layer writes the mean directly: the [K+1, N, d] stack of the reference is never
 //     materialised;
-//   * bf16 storage (LGX_DTYPE_BF16) halves the gathered bytes; arithmetic is fp32 throughout.
+//   * bf16 storage (LGX_DTYPE_BF16) halves the gathered bytes; arithmetic is fp32 throughout;
+//   * optional column blocking of the item rows (lgx_csr cb_*): they gather the large user table,
+//     so they run as a few launches, each over one column range of every item row, whose slice of
+//     the table fits the Infinity Cache; the row sums are carried in an f32 scratch between them.
 #include "lgx_common.h"
 
 namespace lgx {
@@ -119,14 +122,40 @@ struct LayerArgs {
     float n_mean;
     const void* prev[7];  // LGX_LAYER_STACK: the kept layer tables
     int n_prev;
+    // nonzero range of row r: [row_begin[r], row_end[r]) -- indptr / indptr + 1, or the column
+    // block's slice of a blocked row (lgx_csr cb_*)
+    const int64_t* row_begin;
+    const int64_t* row_end;
+    // column-blocked rows: the row sum is carried across the block launches in carry [R, d] f32
+    // (row r at carry + (r - carry_row0) * d): kCarryNone, or store / add (then nothing else) /
+    // take (v = carry + v, then the mode's epilogue)
+    float* carry;
+    int64_t carry_row0;
+    int carry_mode;
 };
 constexpr int kMaxPrev = 7;
+constexpr int kCarryNone = 0, kCarryStore = 1, kCarryAdd = 2, kCarryTake = 3;
 
 // finish one 16-B chunk (VEC values, columns [off, off+VEC)) of output row `row`
 template <typename T>
 __device__ __forceinline__ void finish_chunk(const LayerArgs& a, int64_t row, int64_t off,
                                              float (&v)[Vec<T>::N]) {
     constexpr int VEC = Vec<T>::N;
+    if (a.carry_mode != kCarryNone) {
+        float* cp = a.carry + (row - a.carry_row0) * a.d + off;
+#pragma unroll
+        for (int j = 0; j < VEC; j += 4) {
+            float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (a.carry_mode != kCarryStore) c = *reinterpret_cast<const float4*>(cp + j);
+            if (a.carry_mode == kCarryTake) {
+                v[j] = c.x + v[j]; v[j + 1] = c.y + v[j + 1]; v[j + 2] = c.z + v[j + 2]; v[j + 3] = c.w + v[j + 3];
+            } else {
+                *reinterpret_cast<float4*>(cp + j) =
+                    make_float4(c.x + v[j], c.y + v[j + 1], c.z + v[j + 2], c.w + v[j + 3]);
+            }
+        }
+        if (a.carry_mode != kCarryTake) return;
+    }
     const int64_t o = row * a.d + off;
     switch (a.mode) {
         case LGX_LAYER_PLAIN:
@@ -211,7 +240,7 @@ __global__ __launch_bounds__(kThreads) void spmm_segments(LayerArgs a) {
     const int64_t row = a.seg_row[seg];
     const int part = a.seg_part[seg];
     const int slot = a.seg_slot[seg];
-    const int64_t rb = a.indptr[row], re = a.indptr[row + 1];
+    const int64_t rb = a.row_begin[row], re = a.row_end[row];
     const int64_t b = rb + (int64_t)part * a.seg_len;
     const int64_t e = slot < 0 ? re : min(re, b + a.seg_len);
     const T* __restrict__ X = static_cast<const T*>(a.X);
@@ -406,12 +435,77 @@ int check_csr(const lgx_csr* A, int64_t d, int dtype) {
     const int vec = dtype == LGX_DTYPE_F32 ? 4 : 8;
     LGX_REQUIRE(d > 0 && d % vec == 0 && d <= 1024, LGX_ERR_UNSUPPORTED,
                 "lgx: embedding dim %lld must be a multiple of %d and <= 1024", (long long)d, vec);
-    LGX_REQUIRE(A->n_segs >= A->n_rows, LGX_ERR_INVALID_ARG,
-                "lgx: plan has %lld segments for %lld rows", (long long)A->n_segs, (long long)A->n_rows);
+    const int64_t planned_rows = A->cb_n > 0 ? A->cb_row0 : A->n_rows;
+    LGX_REQUIRE(A->n_segs >= planned_rows, LGX_ERR_INVALID_ARG,
+                "lgx: plan has %lld segments for %lld rows", (long long)A->n_segs, (long long)planned_rows);
     LGX_REQUIRE(A->seg_row && A->seg_part && A->seg_slot, LGX_ERR_INVALID_ARG, "lgx: CSR plan missing");
     LGX_REQUIRE(A->n_split == 0 || (A->split_row && A->split_ptr && A->partials), LGX_ERR_INVALID_ARG,
                 "lgx: split rows need split_row / split_ptr / partials");
     LGX_REQUIRE(A->seg_len > 0, LGX_ERR_INVALID_ARG, "lgx: seg_len must be > 0");
+    if (A->cb_n > 0) {
+        const int64_t R = A->n_rows - A->cb_row0;
+        LGX_REQUIRE(A->cb_row0 >= 0 && R >= 0 && A->cb_ptr && A->cb_plans && (R == 0 || A->cb_carry),
+                    LGX_ERR_INVALID_ARG, "lgx: column blocks need cb_ptr / cb_plans / cb_carry");
+        LGX_REQUIRE(A->n_segs >= A->cb_row0, LGX_ERR_INVALID_ARG, "lgx: plan misses unblocked rows");
+        for (int64_t b = 0; b < A->cb_n; ++b) {
+            const lgx_plan& P = A->cb_plans[b];
+            LGX_REQUIRE(P.n_segs >= R && P.seg_row && P.seg_part && P.seg_slot && P.seg_len > 0 &&
+                            (P.n_split == 0 || (P.split_row && P.split_ptr && P.partials)),
+                        LGX_ERR_INVALID_ARG, "lgx: column block %lld has a bad plan", (long long)b);
+        }
+    } else {
+        LGX_REQUIRE(A->cb_n == 0, LGX_ERR_INVALID_ARG, "lgx: cb_n < 0");
+    }
+    return LGX_OK;
+}
+
+// the plan fields of a LayerArgs from a segment plan
+inline void set_plan(LayerArgs& a, const int32_t* seg_row, const int32_t* seg_part, const int32_t* seg_slot,
+                     int64_t n_segs, int64_t seg_len, const int32_t* split_row, const int32_t* split_ptr,
+                     int64_t n_split, float* partials) {
+    a.seg_row = seg_row;
+    a.seg_part = seg_part;
+    a.seg_slot = seg_slot;
+    a.n_segs = n_segs;
+    a.seg_len = seg_len;
+    a.split_row = split_row;
+    a.split_ptr = split_ptr;
+    a.n_split = n_split;
+    a.partials = partials;
+}
+
+// one layer over every row of A: the unblocked rows in one launch (+ fix-up), then the column
+// blocks in order, the row sums carried between them
+template <typename T>
+int run_layer(const lgx_csr* A, LayerArgs a, hipStream_t stream) {
+    a.indptr = A->indptr;
+    a.indices = A->indices;
+    a.vals = A->vals;
+    a.row_begin = A->indptr;
+    a.row_end = A->indptr + 1;
+    a.carry = nullptr;
+    a.carry_row0 = 0;
+    a.carry_mode = kCarryNone;
+    set_plan(a, A->seg_row, A->seg_part, A->seg_slot, A->n_segs, A->seg_len, A->split_row, A->split_ptr,
+             A->n_split, A->partials);
+    int rc = dispatch_layer<T>(a, stream);
+    if (rc || A->cb_n <= 0) return rc;
+    const int64_t R = A->n_rows - A->cb_row0;
+    if (R == 0) return LGX_OK;
+    a.carry = A->cb_carry;
+    a.carry_row0 = A->cb_row0;
+    for (int64_t b = 0; b < A->cb_n; ++b) {
+        const lgx_plan& P = A->cb_plans[b];
+        set_plan(a, P.seg_row, P.seg_part, P.seg_slot, P.n_segs, P.seg_len, P.split_row, P.split_ptr, P.n_split,
+                 P.partials);
+        // row r of block b: cb_ptr[b R + (r - cb_row0)], indexed by the global row
+        a.row_begin = A->cb_ptr + b * R - A->cb_row0;
+        a.row_end = A->cb_ptr + (b + 1) * R - A->cb_row0;
+        a.carry_mode = A->cb_n == 1 ? kCarryNone
+                       : (b == 0 ? kCarryStore : (b + 1 == A->cb_n ? kCarryTake : kCarryAdd));
+        rc = dispatch_layer<T>(a, stream);
+        if (rc) return rc;
+    }
     return LGX_OK;
 }
 
@@ -435,11 +529,17 @@ extern "C" int lgx_propagate_layer(const lgx_csr* A, const void* X, void* Y, con
                 LGX_ERR_INVALID_ARG, "lgx_propagate_layer: missing buffer for mode %d", mode);
     LGX_REQUIRE(!needOut || n_mean > 0.0f, LGX_ERR_INVALID_ARG, "lgx_propagate_layer: n_mean <= 0");
     if (A->n_rows == 0) return LGX_OK;
-    LayerArgs a{A->indptr, A->indices, A->vals, A->seg_row, A->seg_part, A->seg_slot, A->n_segs,
-                A->seg_len, A->split_row, A->split_ptr, A->n_split, A->partials,
-                X, Y, E0, acc, out, d, mode, n_mean, {}, 0};
-    if (dtype == LGX_DTYPE_F32) return dispatch_layer<float>(a, as_hip(stream));
-    return dispatch_layer<uint16_t>(a, as_hip(stream));
+    LayerArgs a{};
+    a.X = X;
+    a.Y = Y;
+    a.E0 = E0;
+    a.acc = acc;
+    a.out = out;
+    a.d = d;
+    a.mode = mode;
+    a.n_mean = n_mean;
+    if (dtype == LGX_DTYPE_F32) return run_layer<float>(A, a, as_hip(stream));
+    return run_layer<uint16_t>(A, a, as_hip(stream));
 }
 
 extern "C" int lgx_propagate_layer_stack(const lgx_csr* A, const void* X, const void* E0, const void* const* prev,
@@ -454,12 +554,17 @@ extern "C" int lgx_propagate_layer_stack(const lgx_csr* A, const void* X, const 
     for (int p = 0; p < n_prev; ++p)
         LGX_REQUIRE(prev[p], LGX_ERR_INVALID_ARG, "lgx_propagate_layer_stack: prev[%d] is null", p);
     if (A->n_rows == 0) return LGX_OK;
-    LayerArgs a{A->indptr, A->indices, A->vals, A->seg_row, A->seg_part, A->seg_slot, A->n_segs,
-                A->seg_len, A->split_row, A->split_ptr, A->n_split, A->partials,
-                X, nullptr, E0, nullptr, out, d, LGX_LAYER_STACK, n_mean, {}, n_prev};
+    LayerArgs a{};
+    a.X = X;
+    a.E0 = E0;
+    a.out = out;
+    a.d = d;
+    a.mode = LGX_LAYER_STACK;
+    a.n_mean = n_mean;
+    a.n_prev = n_prev;
     for (int p = 0; p < n_prev; ++p) a.prev[p] = prev[p];
-    if (dtype == LGX_DTYPE_F32) return dispatch_layer<float>(a, as_hip(stream));
-    return dispatch_layer<uint16_t>(a, as_hip(stream));
+    if (dtype == LGX_DTYPE_F32) return run_layer<float>(A, a, as_hip(stream));
+    return run_layer<uint16_t>(A, a, as_hip(stream));
 }
 
 namespace lgx {

@@ -29,6 +29,17 @@ from . import _lib
 #    30.7 at 2048 and 30.6 at 16384, tools/spmm_probe.py --phase).
 _SMALL_NNZ = 1 << 24
 
+# Column blocking of the item rows (lgx_csr cb_*): the item rows gather the user table, which at C4
+# is 5.12 GB (f32) / 2.56 GB (bf16), far past the 256 MB Infinity Cache.  Cut into column ranges,
+# each launch gathers one slice of the table, at the price of one pass over every item row per block
+# (segment table, row bounds, partial CSR lines) and an f32 read + write of the carried row sums.
+# tools/cb_probe.py (one MI355X, C4 PLAIN layer, profiles/r03_cb_probe.txt):
+#   f32:  57.24 ms unblocked; 55.10 / 53.58 / 57.63 / 60.66 / 69.51 ms in 4 / 8 / 13 / 16 / 24 blocks
+#   bf16: 28.94 ms unblocked; 28.95 / 29.03 / 34.25 ms in 4 / 8 / 13 blocks
+# so tables of >= 4 GiB are cut into 640 MiB slices (f32 C4: 8 blocks) and smaller ones not at all.
+_CB_TABLE_MIN = 4 << 30
+_CB_SLICE_BYTES = 640 << 20
+
 
 def choose_seg_len(nnz: int) -> int:
     """Segment length: long enough to amortise the fix-up, short enough that hub rows are split
@@ -118,6 +129,9 @@ class CSRGraph:
     n_users: int = 0
     n_items: int = 0
     plan: Optional[Plan] = None
+    col_blocking: bool = True  # column-block the item rows when their gathered table is large
+    col_block_min: int = _CB_TABLE_MIN      # (tests lower these to block small graphs)
+    col_block_slice: int = _CB_SLICE_BYTES
     _dev_plan: dict = field(default_factory=dict, repr=False)
 
     @property
@@ -166,20 +180,102 @@ class CSRGraph:
             self._dev_plan[key] = t
         return t
 
-    def c_struct(self, d: int) -> _lib.LgxCSR:
-        """``struct lgx_csr`` view (device pointers) for an embedding dim d."""
+    def col_block_count(self, d: int, elem_size: int) -> int:
+        """Column blocks of the item rows for tables of d x elem_size-byte rows (0 = none): the
+        square bipartite operator only, when the user table they gather exceeds 1 GiB."""
+        if not self.col_blocking or self.phases() is None or self.n_users < 2:
+            return 0
+        table = self.n_users * d * elem_size
+        if table < self.col_block_min:
+            return 0
+        self.ensure_plan()
+        p = self.plan
+        nu, ns = int(np.count_nonzero(p.seg_row < self.n_users)), int(np.count_nonzero(p.split_row < self.n_users))
+        if not ((p.seg_row[:nu] < self.n_users).all() and (p.split_row[:ns] < self.n_users).all()):
+            return 0  # a plan that is not phased users-first: keep the one-launch layer
+        return int(max(1, min(64, -(-table // self.col_block_slice), self.n_users)))
+
+    def col_blocks(self, nb: int) -> dict:
+        """Block b of item row r covers the nonzeros [ptr[b, r], ptr[b + 1, r]) -- the columns
+        (user ids) in [b U / nb, (b + 1) U / nb) -- with its own launch plan (global row ids).
+        Built once per nb on the device: the (row, column) keys of the item rows are sorted, so
+        every boundary is one searchsorted."""
+        key = ("cb", nb)
+        got = self._dev_plan.get(key)
+        if got is not None:
+            return got
+        self.ensure_plan()
+        U, I, dev = self.n_users, self.n_items, self.device
+        ip = self.indptr
+        s0 = int(ip[U].item())
+        item_ptr = ip[U:U + I + 1]
+        lens = torch.diff(item_ptr)
+        rows = torch.repeat_interleave(torch.arange(I, device=dev, dtype=torch.int64), lens)
+        keys = rows * U + self.indices[s0:].to(torch.int64)
+        del rows
+        cuts = (torch.arange(1, nb, device=dev, dtype=torch.int64) * U) // nb
+        q = (torch.arange(I, device=dev, dtype=torch.int64)[None, :] * U + cuts[:, None]).reshape(-1)
+        inner = (torch.searchsorted(keys, q) + s0).reshape(nb - 1, I)
+        del keys, q
+        ptr = torch.cat([item_ptr[:-1][None, :], inner, item_ptr[1:][None, :]]).contiguous()  # [nb + 1, I]
+        blen = torch.diff(ptr, dim=0).cpu().numpy()
+        plans, dplans = [], []
+        for b in range(nb):
+            ipb = np.zeros(I + 1, dtype=np.int64)
+            np.cumsum(blen[b], out=ipb[1:])
+            pb = make_plan(ipb, self.plan.seg_len)
+            pb.seg_row = (pb.seg_row.astype(np.int64) + U).astype(np.int32)
+            pb.split_row = (pb.split_row.astype(np.int64) + U).astype(np.int32)
+            plans.append(pb)
+            dplans.append({k: torch.from_numpy(getattr(pb, k)).to(dev)
+                           for k in ("seg_row", "seg_part", "seg_slot", "split_row", "split_ptr")})
+        # the unblocked rows (users) are the first phase of the full plan: a prefix of its segments,
+        # split rows and partial slots
+        p = self.plan
+        got = {"ptr": ptr, "plans": plans, "dplans": dplans,
+               "n_user_segs": int(np.count_nonzero(p.seg_row < U)),
+               "n_user_split": int(np.count_nonzero(p.split_row < U))}
+        self._dev_plan[key] = got
+        return got
+
+    def c_struct(self, d: int, elem_size: Optional[int] = None) -> _lib.LgxCSR:
+        """``struct lgx_csr`` view (device pointers) for an embedding dim d; with the storage
+        element size, the item rows are column-blocked when col_block_count says so."""
         self.ensure_plan()
         p, dp = self.plan, self._dev_plan
         part = self.partials(d)
+        nb = self.col_block_count(d, elem_size) if elem_size else 0
+        n_segs, n_split = len(p.seg_row), len(p.split_row)
+        cb = (0, 0, None, None, None)
+        if nb > 0:
+            blk = self.col_blocks(nb)
+            n_segs, n_split = blk["n_user_segs"], blk["n_user_split"]
+            key = ("cb_struct", nb, d)
+            keep = self._dev_plan.get(key)
+            if keep is None:
+                n_part = max(pb.n_partials for pb in blk["plans"])
+                bpart = torch.empty((max(n_part, 1), d), dtype=torch.float32, device=self.device)
+                carry = torch.empty((self.n_items, d), dtype=torch.float32, device=self.device)
+                arr = (_lib.LgxPlan * nb)()
+                for b, (pb, q) in enumerate(zip(blk["plans"], blk["dplans"])):
+                    arr[b] = _lib.LgxPlan(q["seg_row"].data_ptr(), q["seg_part"].data_ptr(), q["seg_slot"].data_ptr(),
+                                          len(pb.seg_row), pb.seg_len,
+                                          q["split_row"].data_ptr() if len(pb.split_row) else None,
+                                          q["split_ptr"].data_ptr(), len(pb.split_row), pb.n_partials,
+                                          bpart.data_ptr() if pb.n_partials else None)
+                keep = self._dev_plan[key] = (arr, bpart, carry)
+            arr, _, carry = keep
+            cb = (self.n_users, nb, blk["ptr"].data_ptr(), arr, carry.data_ptr())
         return _lib.LgxCSR(
             self.indptr.data_ptr(), self.indices.data_ptr(), self.vals.data_ptr(),
             self.n_rows, self.n_cols, self.nnz,
             dp["seg_row"].data_ptr(), dp["seg_part"].data_ptr(), dp["seg_slot"].data_ptr(),
-            len(p.seg_row), p.seg_len,
-            dp["split_row"].data_ptr() if len(p.split_row) else None,
+            n_segs, p.seg_len,
+            dp["split_row"].data_ptr() if n_split else None,
             dp["split_ptr"].data_ptr(),
-            len(p.split_row), p.n_partials,
+            n_split, p.n_partials,
             part.data_ptr() if part is not None else None,
+            *cb,
         )
 
     def to_sparse_coo(self) -> torch.Tensor:

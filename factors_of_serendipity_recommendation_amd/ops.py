@@ -36,7 +36,7 @@ def propagate_layer(A: CSRGraph, X: torch.Tensor, mode: int, Y: Optional[torch.T
     """One LightGCN layer (``lgx_propagate_layer``), writing into caller-provided buffers."""
     require_gpu(X)
     d = X.shape[1]
-    cs = A.c_struct(d)
+    cs = A.c_struct(d, X.element_size())
     _lib.check(_lib.lib().lgx_propagate_layer(ctypes.byref(cs), _ptr(X), _ptr(Y), _ptr(E0), _ptr(acc), _ptr(out),
                                               d, _dtype_code(X), mode, float(n_mean), _stream_ptr(X.device)),
                "lgx_propagate_layer")
@@ -48,7 +48,7 @@ def propagate_layer_stack(A: CSRGraph, X: torch.Tensor, E0: torch.Tensor, prev: 
     out = (E0 + prev[0] + ... + prev[-1] + A X) / n_mean."""
     require_gpu(X, E0, out, *prev)
     d = X.shape[1]
-    cs = A.c_struct(d)
+    cs = A.c_struct(d, X.element_size())
     arr = (ctypes.c_void_p * max(1, len(prev)))(*[p.data_ptr() for p in prev])
     _lib.check(_lib.lib().lgx_propagate_layer_stack(ctypes.byref(cs), _ptr(X), _ptr(E0), arr, len(prev), _ptr(out),
                                                     d, _dtype_code(X), float(n_mean), _stream_ptr(X.device)),
@@ -79,7 +79,7 @@ def spmm(A: CSRGraph, X: torch.Tensor) -> torch.Tensor:
     if X.shape[0] != A.n_cols:
         raise ValueError(f"X has {X.shape[0]} rows, operator has {A.n_cols} columns")
     Y = torch.empty((A.n_rows, X.shape[1]), dtype=X.dtype, device=X.device)
-    cs = A.c_struct(X.shape[1])
+    cs = A.c_struct(X.shape[1], X.element_size())
     _lib.check(_lib.lib().lgx_spmm_csr(ctypes.byref(cs), X.data_ptr(), Y.data_ptr(), X.shape[1], _dtype_code(X),
                                        _stream_ptr(X.device)), "lgx_spmm_csr")
     return Y
@@ -101,7 +101,7 @@ def propagate(A: CSRGraph, E0: torch.Tensor, K: int, out: Optional[torch.Tensor]
     ws = ctypes.c_size_t(0)
     _lib.check(L.lgx_propagate_workspace(N, d, dt, ctypes.byref(ws)), "lgx_propagate_workspace")
     work = torch.empty(max(ws.value, 1), dtype=torch.uint8, device=E0.device)
-    cs = A.c_struct(d)
+    cs = A.c_struct(d, E0.element_size())
     _lib.check(L.lgx_propagate(ctypes.byref(cs), E0.data_ptr(), out.data_ptr(), d, int(K), dt, work.data_ptr(),
                                ws.value, _stream_ptr(E0.device)), "lgx_propagate")
     return out

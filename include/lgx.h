@@ -79,6 +79,20 @@ typedef struct ihipStream_t* lgx_stream_t; /* == hipStream_t */
  *     split_ptr[n_split+1] int32 slot range of each split row
  *     partials [n_partials * d] f32 scratch (may be NULL when n_split == 0)
  */
+/* A segment launch plan (the fields of lgx_csr above, on their own): one per column block. */
+typedef struct lgx_plan {
+    const int32_t* seg_row;   /* row ids of the operator (global rows) */
+    const int32_t* seg_part;
+    const int32_t* seg_slot;
+    int64_t n_segs;
+    int64_t seg_len;
+    const int32_t* split_row;
+    const int32_t* split_ptr;
+    int64_t n_split;
+    int64_t n_partials;
+    float* partials;
+} lgx_plan;
+
 typedef struct lgx_csr {
     const int64_t* indptr;
     const int32_t* indices;
@@ -96,6 +110,21 @@ typedef struct lgx_csr {
     int64_t n_split;
     int64_t n_partials;
     float* partials;
+    /*
+     * Optional column blocking of rows [cb_row0, n_rows) -- the item rows of the bipartite operator,
+     * which gather the (large) user table.  cb_n = 0: none; the plan above covers every row.
+     * cb_n > 0: the plan above covers rows [0, cb_row0) only, and the blocked rows run as cb_n
+     * launches, block b over the nonzeros [cb_ptr[b R + r], cb_ptr[(b + 1) R + r]) of row
+     * cb_row0 + r (R = n_rows - cb_row0; columns ascending, so a block is one range of columns and
+     * its gathers stay inside one slice of the table, small enough for the MALL), each with its
+     * own plan cb_plans[b] (host array; seg_row holds global rows).  Row sums are carried between
+     * the block launches in cb_carry [R, d] f32; the last block adds them and runs the epilogue.
+     */
+    int64_t cb_row0;
+    int64_t cb_n;
+    const int64_t* cb_ptr;      /* [(cb_n + 1) * R] int64, device */
+    const lgx_plan* cb_plans;   /* [cb_n], host */
+    float* cb_carry;            /* [R * d] f32, device */
 } lgx_csr;
 
 const char* lgx_version(void);

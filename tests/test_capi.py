@@ -44,10 +44,28 @@ def test_version_and_error_channel():
         _lib.check(rc, "lgx_topk_rows")
 
 
-def test_lgx_csr_struct_layout_matches_header():
+def test_lgx_csr_struct_layout_matches_header(tmp_path):
+    """The ctypes mirrors of struct lgx_csr / lgx_plan have the header's size and field offsets
+    (compiled from include/lgx.h with the host C compiler)."""
+    import os
+    import subprocess
     from factors_of_serendipity_recommendation_amd import _lib
-    # 16 fields: 9 pointers + 7 int64 -> 128 bytes on LP64
-    assert ctypes.sizeof(_lib.LgxCSR) == 16 * 8
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    fields = [f for f, _ in _lib.LgxCSR._fields_]
+    pfields = [f for f, _ in _lib.LgxPlan._fields_]
+    src = tmp_path / "layout.c"
+    src.write_text("#include <stdio.h>\n#include <stddef.h>\n#include \"lgx.h\"\nint main(void){\n"
+                   + 'printf("%zu %zu\\n", sizeof(lgx_csr), sizeof(lgx_plan));\n'
+                   + "".join(f'printf("%zu\\n", offsetof(lgx_csr, {f}));\n' for f in fields)
+                   + "".join(f'printf("%zu\\n", offsetof(lgx_plan, {f}));\n' for f in pfields)
+                   + "return 0;}\n")
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(root, "include"), str(src), "-o", str(exe)])
+    out = subprocess.check_output([str(exe)]).decode().split()
+    assert int(out[0]) == ctypes.sizeof(_lib.LgxCSR) and int(out[1]) == ctypes.sizeof(_lib.LgxPlan)
+    got = [int(x) for x in out[2:]]
+    want = [getattr(_lib.LgxCSR, f).offset for f in fields] + [getattr(_lib.LgxPlan, f).offset for f in pfields]
+    assert got == want
 
 
 def test_ops_refuse_cpu_tensors():

@@ -263,3 +263,35 @@ def test_vectorised_test_one_batch_equals_reference_loops(seed):
     ref = oracle.torch_style_metrics(pred, truth, [1, 5, 20, 100])
     for key in ("recall", "precision", "ndcg"):
         assert np.array_equal(got[key], ref[key]), key
+
+
+@pytest.mark.parametrize("nb", [1, 3, 8])
+def test_column_blocks_cover_item_rows_once(nb):
+    """CSRGraph.col_blocks: block b of item row r holds exactly the row's nonzeros whose column
+    (user id) lies in [b U / nb, (b + 1) U / nb); every block plan covers every item row once
+    (global row ids); the user rows' plan is the phased plan's prefix."""
+    A, (ip, ix, iv) = _cpu_graph(90, 40, 1500, nb)
+    A.plan = None
+    A.ensure_plan(8)
+    U, I = 90, 40
+    blk = A.col_blocks(nb)
+    ptr = blk["ptr"].numpy()
+    assert ptr.shape == (nb + 1, I)
+    cuts = [(b * U) // nb for b in range(nb + 1)]
+    for r in range(I):
+        row = ip[U + r], ip[U + r + 1]
+        for b in range(nb):
+            cols = ix[ptr[b, r]:ptr[b + 1, r]]
+            assert ((cols >= cuts[b]) & (cols < cuts[b + 1])).all()
+        assert ptr[0, r] == row[0] and ptr[nb, r] == row[1]
+    for b, pb in enumerate(blk["plans"]):
+        lens = np.diff(ptr[b]) if False else ptr[b + 1] - ptr[b]
+        ipb = np.concatenate([[0], np.cumsum(lens)])
+        pb_local = type(pb)(pb.seg_row - U, pb.seg_part, pb.seg_slot, pb.split_row - U, pb.split_ptr, pb.seg_len)
+        _check_plan(ipb, pb_local)
+    p = A.plan
+    assert (p.seg_row[:blk["n_user_segs"]] < U).all() and (p.seg_row[blk["n_user_segs"]:] >= U).all()
+    A.col_block_min, A.col_block_slice = 1, 90 * 4 * 4 // nb + 1
+    assert A.col_block_count(4, 4) == nb
+    cs = A.c_struct(4, 4)
+    assert cs.cb_n == nb and cs.cb_row0 == U and cs.n_segs == blk["n_user_segs"]

@@ -26,6 +26,7 @@ ap.add_argument("--blocks", default="8,20")
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--phase", action="store_true", help="time phase-ordered plans (items then users)")
 ap.add_argument("--hot", default="", help="hot-column set sizes to split off, e.g. 4096,16384")
+ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
 args = ap.parse_args()
 
 from factors_of_serendipity_recommendation_amd import _lib  # noqa: E402
@@ -66,16 +67,18 @@ t0 = time.time()
 A = synth_graph(cfg, seed=2020, device="cuda")
 print(f"graph nnz={A.nnz} in {time.time() - t0:.1f}s seg_len={A.plan.seg_len}", flush=True)
 N = U + I
-E0 = lgx.fill_normal((N, d), 0.1, 2020, dtype=torch.bfloat16)
-Y = torch.empty((N, d), dtype=torch.bfloat16, device="cuda")
+DT = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+ES = 2 if args.dtype == "bf16" else 4
+E0 = lgx.fill_normal((N, d), 0.1, 2020, dtype=DT)
+Y = torch.empty((N, d), dtype=DT, device="cuda")
 acc = torch.zeros((N, d), dtype=torch.float32, device="cuda")
 out = torch.empty((N, d), dtype=torch.float32, device="cuda")
 ms = timed(lambda: ops.propagate_layer(A, E0, _lib.LGX_LAYER_MID, Y=Y, E0=E0, acc=acc, out=out, n_mean=4.0), args.reps)
-report("full layer (MID)", ms, layer_bytes(A.nnz, N, d, 2))
+report("full layer (MID)", ms, layer_bytes(A.nnz, N, d, ES))
 if args.phase:
     from factors_of_serendipity_recommendation_amd.graph import make_plan  # noqa: E402
     ms = timed(lambda: ops.propagate_layer(A, E0, _lib.LGX_LAYER_PLAIN, Y=Y), args.reps)
-    report("full layer (PLAIN)", ms, layer_bytes(A.nnz, N, d, 2))
+    report("full layer (PLAIN)", ms, layer_bytes(A.nnz, N, d, ES))
     ip_host = A.indptr.cpu().numpy()
     for tag, ph in (("items then users", [(U, N), (0, U)]), ("users then items", [(0, U), (U, N)])):
         A.plan = make_plan(ip_host, A.plan.seg_len, phases=ph)
@@ -83,24 +86,24 @@ if args.phase:
         A.ensure_plan()
         for mname, mode in (("PLAIN", _lib.LGX_LAYER_PLAIN), ("MID", _lib.LGX_LAYER_MID)):
             ms = timed(lambda: ops.propagate_layer(A, E0, mode, Y=Y, E0=E0, acc=acc, out=out, n_mean=4.0), args.reps)
-            report(f"phased {tag} ({mname})", ms, layer_bytes(A.nnz, N, d, 2))
+            report(f"phased {tag} ({mname})", ms, layer_bytes(A.nnz, N, d, ES))
     for sl in (8192, 16384, 32768):
         A.plan = make_plan(ip_host, sl, phases=[(0, U), (U, N)])
         A._dev_plan.clear()
         A.ensure_plan()
         ms = timed(lambda: ops.propagate_layer(A, E0, _lib.LGX_LAYER_MID, Y=Y, E0=E0, acc=acc, out=out, n_mean=4.0), args.reps)
-        report(f"phased users/items seg_len {sl} (MID)", ms, layer_bytes(A.nnz, N, d, 2))
+        report(f"phased users/items seg_len {sl} (MID)", ms, layer_bytes(A.nnz, N, d, ES))
 
 sh = make_shard(A, U, I, 0, 1)
 del A, acc, out
 torch.cuda.empty_cache()
 Xi, Xu = E0[U:].contiguous(), E0[:U].contiguous()
-Yu = torch.empty((U, d), dtype=torch.bfloat16, device="cuda")
-Yi = torch.empty((I, d), dtype=torch.bfloat16, device="cuda")
+Yu = torch.empty((U, d), dtype=DT, device="cuda")
+Yi = torch.empty((I, d), dtype=DT, device="cuda")
 ms = timed(lambda: ops.propagate_layer(sh.A_pull, Xi, _lib.LGX_LAYER_PLAIN, Y=Yu), args.reps)
-report("user rows <- item table (A_pull)", ms, layer_bytes(sh.A_pull.nnz, U, d, 2))
+report("user rows <- item table (A_pull)", ms, layer_bytes(sh.A_pull.nnz, U, d, ES))
 ms = timed(lambda: ops.propagate_layer(sh.A_push, Xu, _lib.LGX_LAYER_PLAIN, Y=Yi), args.reps)
-report("item rows <- user table (A_push)", ms, layer_bytes(sh.A_push.nnz, I, d, 2))
+report("item rows <- user table (A_push)", ms, layer_bytes(sh.A_push.nnz, I, d, ES))
 
 
 
@@ -129,8 +132,8 @@ for name, G, X, n_out in (("A_pull", sh.A_pull, Xi, U), ("A_push", sh.A_push, Xu
         torch.cuda.synchronize()
         ms_h = timed(lambda: ops.propagate_layer(hot, X, _lib.LGX_LAYER_PARTIAL, out=outb), args.reps)
         ms_c = timed(lambda: ops.propagate_layer(cold, X, _lib.LGX_LAYER_PARTIAL, out=outb), args.reps)
-        report(f"{name} hot {H} cols ({hot.nnz / G.nnz:.2f} of nnz)", ms_h, layer_bytes(hot.nnz, n_out, d, 2, 4))
-        report(f"{name} cold rest", ms_c, layer_bytes(cold.nnz, n_out, d, 2, 4))
+        report(f"{name} hot {H} cols ({hot.nnz / G.nnz:.2f} of nnz)", ms_h, layer_bytes(hot.nnz, n_out, d, ES, 4))
+        report(f"{name} cold rest", ms_c, layer_bytes(cold.nnz, n_out, d, ES, 4))
         del hot, cold
         torch.cuda.empty_cache()
     del outb
@@ -156,7 +159,7 @@ for nb in [int(x) for x in args.blocks.split(",") if x]:
             ops.propagate_layer(g, Xu, _lib.LGX_LAYER_PARTIAL, out=Pout)
 
     ms = timed(run, args.reps)
-    report(f"A_push in {nb} user-column blocks", ms, layer_bytes(P.nnz, I, d, 2))
+    report(f"A_push in {nb} user-column blocks", ms, layer_bytes(P.nnz, I, d, ES))
     del subs
     torch.cuda.empty_cache()
 print("probe done", flush=True)
