@@ -58,10 +58,21 @@ def main():
                 w = csv.DictWriter(fh, fieldnames=list(rows[0].keys()))
                 w.writeheader()
                 w.writerows(rows)
-        for r in rows:
+        # legs: the propagation kernels by storage type; the scoring sweeps by kernel (f32 leg:
+        # score_topk_f32_lds, bf16 leg: score_topk_bf16_lds); a finalize belongs to the leg of the
+        # sweep dispatched before it
+        last_scoring = "scoring"
+        for r in sorted(rows, key=lambda r: int(r.get("Dispatch_Id", 0) or 0)):
             name = r["Kernel_Name"]
             k = short(name)
-            leg = "scoring" if "score" in k else ("bf16" if "unsigned short" in name else "f32")
+            if k == "score_topk_f32_lds":
+                leg = last_scoring = "scoring_f32"
+            elif k == "score_topk_bf16_lds":
+                leg = last_scoring = "scoring"
+            elif "score" in k:
+                leg = last_scoring
+            else:
+                leg = "bf16" if "unsigned short" in name else "f32"
             per[(leg, k)][counter].append(float(r["Counter_Value"]))
     kernels = defaultdict(dict)
     for (leg, k), v in per.items():
@@ -73,8 +84,8 @@ def main():
                            "hbm_bytes_per_launch": (2 * f + w) * 1024}
     import hashlib
     h = hashlib.sha256(open(os.path.join(ROOT, "factors_of_serendipity_recommendation_amd", "liblgx.so"), "rb").read())
-    doc = {"workload": f"{config} (bench.py default: propagation K=3 d=128 bf16 and f32 + scoring d=256 bf16, "
-                       "1M items), n_gpus=1",
+    doc = {"workload": f"{config} (bench.py default: propagation K=3 d=128 f32 and bf16 + scoring d=256 f32 "
+                       "(262144 users) and bf16 (1M users), 1M items), n_gpus=1",
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (tools/profile_round.sh); "
                      "bytes = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024, the x2 measured for streaming reads and for "
                      "random 256-B / 512-B row gathers (profiles/r02_fetch_calibration.json). FETCH_SIZE counts "

@@ -11,8 +11,8 @@ ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS="--steps 3 --warmup 1 --fp32-steps 2 --no-cpu-baseline"
-KRE='spmm_segments|spmm_fixup|score_topk_bf16_lds|score_topk_finalize'
+ARGS="--steps 3 --warmup 1 --extra-steps 2 --score-steps 1 --no-cpu-baseline"
+KRE='spmm_segments|spmm_fixup|score_topk_bf16_lds|score_topk_f32_lds|score_topk_finalize'
 echo "[profile] plain bench"
 timeout -k 10 900 python3 "$ROOT/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.log"
 cd /tmp
