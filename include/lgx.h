@@ -22,6 +22,7 @@
  *   lgx_score_topk         Procedure.Test mask + torch.topk     code/Procedure.py:127-135;
  *                          batch_test.test mask + evaluator     LightGCN-tf/utility/batch_test.py:47-70
  *                          recommend.py global min/max          recommend.py:163-164, 375-377
+ *   lgx_score_minmax       np.max / np.min of the U x I dot     recommend.py:163-164, 377; utils.py:500-529
  *   lgx_topk_rows          c_top_k_array_index                  LightGCN-tf/evaluator/cpp/include/tools.h:13-33
  *   lgx_foldout_metrics    evaluate_foldout                     LightGCN-tf/evaluator/cpp/include/evaluate_foldout.h:115-195
  *   lgx_gather_scores      accuracy_cf / elasticity_item per-user candidate dot  recommend.py:167-171, 214-217
