@@ -153,11 +153,22 @@ __device__ __forceinline__ int tile_row(int r, int h) { return (r & 3) + 8 * (r 
 // writes once its real slots are full)
 __host__ __device__ constexpr int kstride(int k) { return (k + 1) & ~1; }
 constexpr int kListSpare = 8;  // the 8-key rescan of user 31 may read past its row
+// deferred slots per lane: 4 in the register-fragment and fp32 LDS kernels; 12 in the bf16 LDS kernel,
+// whose events are 16x more frequent per MFMA cycle: a lane overflows its slots (and sends the
+// wave down the exact path) 3x less often.  tools/score_lab (131072 users x 1M items, d=256,
+// profiles/r03_score_lab_pend.txt): 4 slots + 3 ring buffers 59.50 ms over the 7 seeded stages,
+// 1073 TF/s masked one-sweep; 4 slots + 2 buffers 60.18 ms; 8 slots 58.29 ms, 1103; 12 slots
+// 57.75 ms, 1103 (1168 unmasked, +4 %).  12 slots take the LDS of the third ring buffer (the
+// ring's depth measured neutral) and fit d = 256 up to k = 20.
 constexpr int kPendSlots = 4;
+#ifndef LGX_PEND_SLOTS_LDS
+#define LGX_PEND_SLOTS_LDS 12
+#endif
+constexpr int kPendBf16Lds = LGX_PEND_SLOTS_LDS;
 __host__ __device__ constexpr size_t list_keys_per_wave(int k) { return (size_t)kUsersPerWave * kstride(k) + kListSpare; }
 // ... then one int per lane: the count of its parked keys (kSuspSlots)
-__host__ __device__ constexpr size_t list_bytes_per_wave(int k) {
-    return (list_keys_per_wave(k) + 64 * (kPendSlots + 1)) * 8 + 64 * 4;
+__host__ __device__ constexpr size_t list_bytes_per_wave(int k, int pend = kPendSlots) {
+    return (list_keys_per_wave(k) + 64 * (pend + 1)) * 8 + 64 * 4;
 }
 
 // value held by lane (lane ^ 32): one v_permlane32_swap, no LDS traffic
@@ -172,7 +183,8 @@ __device__ __forceinline__ uint32_t other_half(uint32_t x) {
 // The lane mirrors the worst kept entry (tau, tau_i) for the per-score filter.  An accepted
 // candidate overwrites the worst entry and the new worst is found by one scan of k independent
 // LDS reads -- no dependent shift chain.  Lists are sorted only when merged.
-struct WaveTopK {
+template <int PEND>
+struct WaveTopKT {
     uint64_t* keys;  // this lane's user: [k]
     int k, h;
     int64_t b;       // query index of this lane's user
@@ -181,8 +193,8 @@ struct WaveTopK {
     uint64_t kmin;   // worst kept key (valid when len == k)
     // deferred candidates of THIS lane (its half's items), inserted into the list in batches so
     // that a late-sweep survivor costs a few register moves instead of LDS round trips
-    static constexpr int kPend = kPendSlots;
-    static_assert(kPend == 4, "drop_masked's lockstep search is written for 4 slots");
+    static constexpr int kPend = PEND;
+    static_assert(kPend >= 1 && kPend <= 16, "deferred slots: 1..16 per lane");
     LGX_STAT_DECL
     // this lane's kPend (+1 scratch) slots in LDS; a slot holds the raw pair (score bits, item << 32)
     uint64_t* pend;
@@ -552,7 +564,13 @@ struct WaveTopK {
             hi[j] = (need >> j) & 1u ? (int32_t)(m1 - m0) : 0;
         }
         // first index with mi[idx] >= it, for every needed key at once
-        while (__ballot(((need != 0u) & ((lo[0] < hi[0]) | (lo[1] < hi[1]) | (lo[2] < hi[2]) | (lo[3] < hi[3])))) != 0ull) {
+        auto searching = [&]() {
+            bool any = false;
+#pragma unroll
+            for (int j = 0; j < kPend; ++j) any |= lo[j] < hi[j];
+            return (need != 0u) & any;
+        };
+        while (__ballot(searching()) != 0ull) {
             int32_t v[kPend];
 #pragma unroll
             for (int j = 0; j < kPend; ++j) v[j] = lo[j] < hi[j] ? mi[(lo[j] + hi[j]) >> 1] : 0;
@@ -687,6 +705,7 @@ struct WaveTopK {
         }
     }
 };
+typedef WaveTopKT<kPendSlots> WaveTopK;
 
 
 template <int DT, int KCH, bool MINMAX, int WPB>
@@ -829,7 +848,11 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     // SKIP: the fast-path test runs on the MFMA output layout itself (lane l holds 16 scores of user
     // l & 15 and 16 of user 16 + (l & 15)); the regroup into the top-k layout (16 v_permlane16_swap)
     // is paid only by tiles that have a survivor.  Min / max needs every score: not with MINMAX.
-    constexpr bool SKIP = FASTSKIP && M16 && !MINMAX && (ABLATE == 0 || ABLATE == 9);
+    // development ablations 11 / 12 (tools/score_lab LAB_ABL): 11 = an event is detected and then
+    // dropped (fast path + detection only), 12 = events take the deferred-slot path and the slots are
+    // discarded instead of drained (no drains, no exact path) -- timing only, the lists are wrong
+    constexpr bool LIKE_PRODUCT = ABLATE == 0 || ABLATE == 9 || ABLATE == 11 || ABLATE == 12;
+    constexpr bool SKIP = FASTSKIP && M16 && !MINMAX && LIKE_PRODUCT;
     constexpr bool DIRECT_EVENTS = LGX_DIRECT_EVENTS != 0;
     typedef LdsGeom<KSTEPS, WAVES, NACC, F32 ? 4 : 2> G;
     typedef Frag<DT> F;
@@ -840,7 +863,8 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5, col = lane & 31;
-    uint64_t* lk = reinterpret_cast<uint64_t*>(smem + (size_t)nbuf * G::TILE + (size_t)wave * list_bytes_per_wave(k));
+    typedef WaveTopKT<F32 ? kPendSlots : kPendBf16Lds> TopK;
+    uint64_t* lk = reinterpret_cast<uint64_t*>(smem + (size_t)nbuf * G::TILE + (size_t)wave * list_bytes_per_wave(k, TopK::kPend));
 
     // workgroup -> (catalog split, user tile)
     const int64_t bid = blockIdx.x;
@@ -876,7 +900,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
 #pragma unroll
         for (int c = 0; c < KSTEPS; ++c) uf[c] = __builtin_bit_cast(uint4, F::load(a.Q, qrow, a.d, c, h, user_ok));
     }
-    WaveTopK st;
+    TopK st;
     st.init(lk, lk + list_keys_per_wave(k), k, lane, b, user_ok);
     st.enable_suspects(a);
     st.build_bloom(a);
@@ -944,7 +968,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(ahead, ntiles) - 1));
     __syncthreads();
     int buf = 0, sbuf = ahead;  // buffer of tile t / of tile t + ahead
-    const bool late = STAGGER && (ABLATE == 0 || ABLATE == 9) && wave >= WAVES / 2;  // wave-uniform
+    const bool late = STAGGER && LIKE_PRODUCT && wave >= WAVES / 2;  // wave-uniform
     f32x16 acc0, acc1;  // late waves: tile t-1's scores, held across the barrier
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     f32x4 c[2][4];      // 16x16x32 accumulators: c[ub][ib] = items 16 ib + 4 (lane >> 4) + reg, user 16 ub + (lane & 15)
@@ -1104,6 +1128,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
                         m1 = fmaxf(m1, c[1][ib][r]);
                     }
                 if (__ballot((m0 >= tauA) | (m1 >= tauB)) == 0ull) return;  // wave-uniform fast path
+                if constexpr (ABLATE == 11) return;
                 // maxima of one item block's 4-score groups (both user blocks), re-derived on events
                 auto flagged = [&](int ib) {
                     const float a0 = fmaxf(fmaxf(c[0][ib][0], c[0][ib][1]), fmaxf(c[0][ib][2], c[0][ib][3]));
@@ -1127,14 +1152,18 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
                             const auto sw = __builtin_amdgcn_permlane16_swap(
                                 __float_as_uint(c[0][ib][reg]), __float_as_uint(c[1][ib][reg]), false, false);
                             const uint32_t it = ibase + 16 * ib + reg;
-                            st.pend[min(n, WaveTopK::kPend)] = ((uint64_t)it << 32) | sw[0];
+                            st.pend[min(n, TopK::kPend)] = ((uint64_t)it << 32) | sw[0];
                             n += __uint_as_float(sw[0]) >= st.tau ? 1 : 0;
-                            st.pend[min(n, WaveTopK::kPend)] = ((uint64_t)(it + 4) << 32) | sw[1];
+                            st.pend[min(n, TopK::kPend)] = ((uint64_t)(it + 4) << 32) | sw[1];
                             n += __uint_as_float(sw[1]) >= st.tau ? 1 : 0;
                         }
                     }
-                    if (__ballot(n > WaveTopK::kPend) == 0ull) {
+                    if (__ballot(n > TopK::kPend) == 0ull) {
                         st.pcnt = n;
+                        return;
+                    }
+                    if constexpr (ABLATE == 12) {
+                        st.pcnt = 0;
                         return;
                     }
                 }
@@ -1677,10 +1706,13 @@ inline int64_t lds_resident() { return 256; }
 constexpr size_t kLdsBytes = 160 * 1024;
 constexpr int kTileItems = 64;
 // LDS kernel applies to bf16 with d a multiple of 32 up to 256 (even k-step counts are
-// instantiated) and k <= 32; to f32 with d a multiple of 64 up to 256 when two 64-item tiles fit
-// beside the 4 waves' top-k lists (d = 256: k <= 20)
+// instantiated) and to f32 with d a multiple of 64 up to 256, whenever two 64-item tiles fit beside
+// the top-k lists (8 waves with 12 deferred slots per lane / 4 waves with 4): d = 256 up to k = 20
+// (both dtypes), bf16 d <= 128 up to k = 32; other shapes run the register-fragment kernel
 bool lds_eligible(int dtype, int64_t d, int k) {
-    if (dtype == LGX_DTYPE_BF16) return d % 32 == 0 && d >= 32 && d <= 256 && k <= 32;
+    if (dtype == LGX_DTYPE_BF16)
+        return d % 32 == 0 && d >= 32 && d <= 256 && k <= 32 &&
+               2 * (size_t)kTileItems * d * 2 + 8 * list_bytes_per_wave(k, kPendBf16Lds) <= kLdsBytes;
     if (dtype != LGX_DTYPE_F32 || d % 64 != 0 || d < 64 || d > 256 || k > 32) return false;
     return 2 * (size_t)kTileItems * d * 4 + (size_t)kF32LdsWaves * list_bytes_per_wave(k) <= kLdsBytes;
 }
@@ -1760,6 +1792,9 @@ int launch_v1(const ScoreArgs& a, int kch, hipStream_t stream) {
 // tile buffers of the LDS kernel: as many as fit beside the top-k lists in the workgroup's share of
 // the CU's LDS, 2..4
 inline int lds_ring_buffers(size_t tile, size_t lists, int wg_per_cu) {
+#ifdef LGX_LAB_NBUF  // development A/B (tools/Makefile score_lab_nb2): a fixed ring depth
+    return LGX_LAB_NBUF;
+#endif
     const size_t budget = kLdsBytes / wg_per_cu;
     const size_t fit = lists < budget ? (budget - lists) / tile : 0;
     return (int)std::max<size_t>(2, std::min<size_t>(4, fit));
@@ -1768,7 +1803,7 @@ inline int lds_ring_buffers(size_t tile, size_t lists, int wg_per_cu) {
 template <int KS, bool MM, int ABL, int WAVES, int NACC, bool STAGGER, bool M16, int DMAPOS = 0, bool SKIP = true>
 int launch_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     typedef LdsGeom<KS, WAVES, NACC> G;
-    const size_t lists = (size_t)WAVES * list_bytes_per_wave(a.k);
+    const size_t lists = (size_t)WAVES * list_bytes_per_wave(a.k, kPendBf16Lds);
     const int nbuf = lds_ring_buffers(G::TILE, lists, 1);
     const size_t shmem = (size_t)nbuf * G::TILE + lists;
     int rc = set_lds_limit(score_topk_bf16_lds<KS, MM, ABL, WAVES, NACC, STAGGER, M16, DMAPOS, SKIP>, shmem);

@@ -203,7 +203,8 @@ def test_seeded_full_sweep_equals_one_sweep():
     assert (got >= kth - 1e-5 * kth.abs().clamp(min=1.0)).all()
 
 
-@pytest.mark.parametrize("d,k,rows", [(64, 1, False), (128, 7, True), (256, 32, False), (96, 20, True)])
+@pytest.mark.parametrize("d,k,rows", [(64, 1, False), (128, 7, True), (128, 32, False), (256, 20, True),
+                                      (96, 20, True)])
 def test_seeded_sweep_shapes(d, k, rows):
     """The seeded stages across the LDS kernel's shapes (d, k) and with user_rows: lists equal, as
     sets, the one-launch sweep of the unseeded min/max variant."""

@@ -270,6 +270,13 @@ int main(int argc, char** argv) {
             std::printf("3 stages S1=%lld S=%lld: %.2f + %.2f + %.2f = %.2f ms; %lld users differ\n", (long long)S1,
                         (long long)S, u[0], u[1], u[2], u[0] + u[1] + u[2], (long long)bad);
         }
+    } else if (getenv("LAB_EVT")) {  // where the top-k time goes: events dropped, slots never drained
+        for (int masked = 0; masked <= 1; ++masked) {
+            if (timeit("full", launch<0, 0>, masked)) return 1;
+            if (timeit("fast path only (tau = +inf)", launch<9, 0>, masked)) return 1;
+            if (timeit("events detected, dropped", launch<11, 0>, masked)) return 1;
+            if (timeit("deferred slots, never drained", launch<12, 0>, masked)) return 1;
+        }
     } else if (getenv("LAB_ABL")) {  // the MFMA / LDS-read / refill ladder (unmasked)
         if (timeit("full", launch<0, 0>, false)) return 1;
         if (timeit("no-topk", launch<1, 0>, false)) return 1;
