@@ -131,6 +131,54 @@ int main(int argc, char** argv) {
         }
         std::printf("B=%lld + tail %lld (splits %d): stages then tail %.2f ms (tail alone %.2f) | tail beside the stages %.2f ms (%.1f %%)\n",
                     (long long)B, (long long)T, pt.n_splits, seq, tl, conc, 100.0 * (seq - conc) / seq);
+    } else if (getenv("LAB_STAGEPROF")) {  // the product's seeded stages, each timed after its predecessors ran
+        // untimed (so its seed is what the chain hands it), vs the same stage with tau = +inf (fast path only)
+        std::vector<int64_t> cut;
+        for (int64_t hi = 16384; 3 * hi < 2 * I; hi *= 2) cut.push_back(hi);
+        cut.push_back(I);
+        const bool um = getenv("LAB_UNMASKED") != nullptr;
+        uint64_t* susp = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + (size_t)B * p.n_splits * k * 8);
+        float* ps = reinterpret_cast<float*>(ws);
+        int32_t* pi = reinterpret_cast<int32_t*>(static_cast<char*>(ws) + (size_t)B * k * 4);
+        SplitPlan q = p;
+        q.n_splits = 1;
+        std::vector<ScoreArgs> st;
+        for (size_t j = 0; j < cut.size(); ++j) {
+            const int64_t lo = j ? cut[j - 1] : 0;
+            ScoreArgs x{Q, nullptr, items, B, cut[j], d, um ? nullptr : mp, um ? nullptr : mi, k, 1, cut[j] - lo, ps, pi, nullptr, susp,
+                        j ? ps : nullptr, j ? pi : nullptr, lo};
+            st.push_back(x);
+        }
+        double tot = 0, totf = 0;
+        for (size_t j = 0; j < st.size(); ++j) {
+            float best = 1e30f, bestf = 1e30f;
+            for (int r = 0; r < 3; ++r) {
+                for (size_t i = 0; i < j; ++i)
+                    if (launch<0, 0>(st[i], q, nullptr)) return 1;
+                float ms;
+                HK(hipEventRecord(e0, nullptr));
+                if (launch<0, 0>(st[j], q, nullptr)) return 1;
+                HK(hipEventRecord(e1, nullptr));
+                HK(hipEventSynchronize(e1));
+                HK(hipEventElapsedTime(&ms, e0, e1));
+                best = std::min(best, ms);
+                HK(hipEventRecord(e0, nullptr));
+                if (launch<9, 0>(st[j], q, nullptr)) return 1;
+                HK(hipEventRecord(e1, nullptr));
+                HK(hipEventSynchronize(e1));
+                HK(hipEventElapsedTime(&ms, e0, e1));
+                bestf = std::min(bestf, ms);
+            }
+            const double fl = 2.0 * B * st[j].split_items * d;
+            std::printf("stage [%7lld, %7lld) %8.3f ms %6.0f TF/s | fast path only %8.3f ms %6.0f TF/s | events +%.3f ms\n",
+                        (long long)st[j].seed_items, (long long)cut[j], best, fl / (best * 1e-3) / 1e12, bestf,
+                        fl / (bestf * 1e-3) / 1e12, best - bestf);
+            std::fflush(stdout);
+            tot += best;
+            totf += bestf;
+        }
+        std::printf("stages%s: %.2f ms, fast path only %.2f ms (%.0f vs %.0f TF/s)\n", um ? " (unmasked)" : "", tot, totf,
+                    2.0 * B * I * d / (tot * 1e-3) / 1e12, 2.0 * B * I * d / (totf * 1e-3) / 1e12);
     } else if (getenv("LAB_STAGES")) {  // seeded stages at the given item boundaries (comma list), vs one sweep
         std::vector<int64_t> cut;
         for (const char* c = getenv("LAB_STAGES"); *c;) {
