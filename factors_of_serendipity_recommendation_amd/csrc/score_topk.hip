@@ -120,6 +120,10 @@ struct ScoreArgs {
     const float* seed_score;
     const int32_t* seed_idx;
     int64_t seed_items;
+    // score floor [B, n_splits] (LDS kernel): written by the kFloorOnly walk over the first
+    // floor_items items of each split, read by an unseeded sweep as every list's starting threshold
+    float* floor;
+    int64_t floor_items;
 };
 
 // Candidates whose mask test the Bloom filter cannot settle ("suspects", ~10 % of the survivors) are
@@ -423,17 +427,21 @@ struct WaveTopKT {
         return make_key(__uint_as_float((uint32_t)v), pend_item(v));
     }
 
+    // true while some lane's filter admits every score: a list still filling with no floor under it
+    // (the sweep's first block); such a wave takes the exact path, deferring would overflow at once
+    __device__ __forceinline__ bool unbounded() const { return len < k && tau == -INFINITY; }
+
     template <int NACC, bool L16>
     __device__ __forceinline__ void slow(const ScoreArgs& a, const f32x16& acc0, const f32x16& acc1, const float* g,
                                          int64_t ib, int32_t rem) {
-        // Every list full: each score >= tau of a group some lane flagged is appended to this lane's
-        // deferred slots without branching -- an unconditional 8-B LDS write to slot min(n, kPend)
-        // and n += (score >= tau) -- so an event costs a few instructions per score whatever the
-        // lanes do.  Ties at tau and masked items are sorted out when the slots are drained (exact
-        // key compare, mask test).  A lane that runs past its slots (n > kPend) sends the whole
-        // block down the exact path instead: drain, then insert every survivor directly.  A list
-        // still filling (first block) takes that path too.
-        if (__ballot(len < k) == 0ull) {
+        // Every filter bounded (full lists, or filling lists above their floor): each score >= tau of
+        // a group some lane flagged is appended to this lane's deferred slots without branching -- an
+        // unconditional 8-B LDS write to slot min(n, kPend) and n += (score >= tau) -- so an event
+        // costs a few instructions per score whatever the lanes do.  Ties at tau and masked items are
+        // sorted out when the slots are drained (exact key compare, mask test).  A lane that runs past
+        // its slots (n > kPend) sends the whole block down the exact path instead: drain, then insert
+        // every survivor directly.  An unbounded filter takes that path too.
+        if (__ballot(unbounded()) == 0ull) {
             int n = pcnt;
 #pragma unroll
             for (int q = 0; q < 2 * NACC; ++q) {
@@ -487,6 +495,7 @@ struct WaveTopKT {
     template <int NACC, bool L16>
     __device__ __forceinline__ uint32_t survivors(const f32x16& acc0, const f32x16& acc1, int64_t ib,
                                                   int32_t rem) const {
+        // a filling list takes every score at or above its floor (tau: -inf without one)
         const bool notfull = len < k;
         const int64_t l64 = (int64_t)tau_i - ib;
         const int32_t lim = l64 > (1 << 30) ? (1 << 30) : l64 < -1 ? -1 : (int32_t)l64;
@@ -497,7 +506,7 @@ struct WaveTopKT {
             for (int r = 0; r < 16; ++r) {
                 const float sc = j ? acc1[r] : acc0[r];
                 const int32_t off = row_off<L16>(j, r);
-                const bool beats = notfull | (sc > tau) | ((sc == tau) & (off < lim));
+                const bool beats = (notfull & (sc >= tau)) | (sc > tau) | ((sc == tau) & (off < lim));
                 cmask |= (user_ok & (off < rem) & beats) ? (1u << (16 * j + r)) : 0u;
             }
         }
@@ -761,6 +770,14 @@ __global__ __launch_bounds__(WPB * 64) void score_topk_kernel(ScoreArgs a) {
 // touched): lgx_score_minmax, the reference's np.max / np.min over the full U x I matrix
 // (recommend.py:163-164, :377).  A product mode, not a development ablation.
 constexpr int kMinMaxOnly = 10;
+// ABLATE value of the walk that writes each user's score floor (ScoreArgs::floor) over the first
+// floor_items items of its split instead of a top-k: the items are cut into 64 groups by their
+// position in the 64-item tile, a group holding a masked item of the user is dropped, and the floor
+// is the k-th largest of the remaining group maxima.  Those are k distinct unmasked items scoring
+// at least the floor, so the user's k-th best (over the split, hence over the catalog) is never below
+// it, and a sweep that starts its lists with this threshold drops no item of the exact top-k (ties
+// at the floor included: a filling list takes scores >= floor).  A product mode.
+constexpr int kFloorOnly = 13;
 
 template <int KSTEPS, int WAVES = 8, int NACC = 2, int ESZ = 2>
 struct LdsGeom {
@@ -905,6 +922,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     st.enable_suspects(a);
     st.build_bloom(a);
     if (a.seed_score) st.seed(a);
+    else if (ABLATE != kFloorOnly && a.floor && user_ok) st.tau = a.floor[b * a.n_splits + split];
     // consume the prologue loads here: otherwise the compiler treats them as possibly pending at
     // the loop header and waits vmcnt(0) -- i.e. for the tile prefetch -- in every iteration
 #pragma unroll
@@ -917,7 +935,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     for (int w = 0; w < kBloomWords; ++w) asm volatile("" : "+v"(st.bl[w]));
 
     const int64_t i_begin = a.seed_items + (int64_t)split * a.split_items;
-    const int64_t i_end = min(a.n_items, i_begin + a.split_items);
+    const int64_t i_end = min(a.n_items, i_begin + (ABLATE == kFloorOnly ? min(a.split_items, a.floor_items) : a.split_items));
     const int64_t ntiles = i_end > i_begin ? (i_end - i_begin + G::TILE_ITEMS - 1) / G::TILE_ITEMS : 0;
     // single split: every workgroup sweeps the whole catalog, starting at a rotation shared by the
     // workgroups of its XCD (blockIdx mod 8) so that co-resident workgroups read the same tiles
@@ -1056,7 +1074,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
                     if (s2 + 1 < KS2) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 }
             }
-            if (!SKIP && ABLATE != kMinMaxOnly) regroup();
+            if (!SKIP && ABLATE != kMinMaxOnly && ABLATE != kFloorOnly) regroup();
         } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -1111,9 +1129,32 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         st.mn = fminf(st.mn, fminf(uok0 ? lo0 : INFINITY, uok1 ? lo1 : INFINITY));
         st.mx = fmaxf(st.mx, fmaxf(uok0 ? hi0 : -INFINITY, uok1 ? hi1 : -INFINITY));
     };
+    // floor mode: running maxima per (user, position in the tile), in the MFMA layout: gm[ub][ib][r]
+    // = group 16 ib + 4 q4 + r of user 16 ub + r16.  Positions past the split's end (the tail tile's
+    // re-read rows) stay out.
+    f32x4 gm[2][4];
+#pragma unroll
+    for (int ub = 0; ub < 2; ++ub)
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib) gm[ub][ib] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    auto floor_tile = [&](int64_t e0) {
+        const int64_t rem = i_end - e0;
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const bool in = 16 * ib + 4 * q4 + r < rem;
+                gm[0][ib][r] = in ? fmaxf(gm[0][ib][r], c[0][ib][r]) : gm[0][ib][r];
+                gm[1][ib][r] = in ? fmaxf(gm[1][ib][r], c[1][ib][r]) : gm[1][ib][r];
+            }
+    };
     auto epilogue = [&](int64_t e0) {
         if constexpr (ABLATE == kMinMaxOnly) {
             minmax_tile();
+            return;
+        }
+        if constexpr (ABLATE == kFloorOnly) {
+            floor_tile(e0);
             return;
         }
         const bool tail = e0 + G::TILE_ITEMS > i_end;
@@ -1135,13 +1176,14 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
                     const float a1 = fmaxf(fmaxf(c[1][ib][0], c[1][ib][1]), fmaxf(c[1][ib][2], c[1][ib][3]));
                     return __ballot((a0 >= tauA) | (a1 >= tauB)) != 0ull;
                 };
-                // Every list full (the sweep past its first tiles): defer the flagged item blocks'
+                // Every filter bounded (the sweep past its first tiles, or lists filling above their
+                // floor): defer the flagged item blocks'
                 // scores straight from the MFMA layout -- 4 v_permlane16_swap per block bring a
                 // user's 8 scores of that block to its own lanes -- instead of regrouping all 32
                 // scores and re-deriving the group maxima.  A lane whose slots would run over goes
                 // down the full path below, which re-appends from pcnt (the writes here only went
                 // to slots at or past it).
-                if (DIRECT_EVENTS && __ballot(st.len < st.k) == 0ull) {
+                if (DIRECT_EVENTS && __ballot(st.unbounded()) == 0ull) {
                     int n = st.pcnt;
                     const uint32_t ibase = (uint32_t)(e0 + 8 * h);
 #pragma unroll
@@ -1244,6 +1286,56 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         if (lane == 0 && st.mn <= st.mx) {
             atomicMin(a.minmax, ord_f32(st.mn));
             atomicMax(a.minmax + 1, ord_f32(st.mx));
+        }
+        return;
+    }
+    if constexpr (ABLATE == kFloorOnly) {
+#pragma unroll
+        for (int ub = 0; ub < 2; ++ub) {
+            const int64_t bu = utile * G::USERS + wave * kUsersPerWave + 16 * ub + r16;
+            const bool ok = bu < a.B;
+            // drop the groups that hold a masked item of the user (the mask rows are sorted)
+            if (a.mask_indptr && ok) {
+                const int64_t m1 = a.mask_indptr[bu + 1];
+                for (int64_t j = a.mask_indptr[bu]; j < m1; ++j) {
+                    const int64_t it = a.mask_indices[j];
+                    if (it >= i_end) break;
+                    if (it < i_begin) continue;
+                    const int pos = (int)((it - i_begin) & 63);
+                    if (((pos >> 2) & 3) != q4) continue;
+#pragma unroll
+                    for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            if (pos == 16 * ib + 4 * q4 + r) gm[ub][ib][r] = -INFINITY;
+                }
+            }
+            // k-th largest of the user's 64 group maxima (4 lanes q4 x 16 registers): k rounds of
+            // take the maximum, then remove one copy of it (from the lowest q4 holding it)
+            float kth = -INFINITY;
+            for (int round = 0; round < k; ++round) {
+                float lm = gm[ub][0][0];
+#pragma unroll
+                for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) lm = fmaxf(lm, gm[ub][ib][r]);
+                float wm = fmaxf(lm, __shfl_xor(lm, 16, 64));
+                wm = fmaxf(wm, __shfl_xor(wm, 32, 64));
+                int owner = lm == wm ? q4 : 4;
+                owner = min(owner, __shfl_xor(owner, 16, 64));
+                owner = min(owner, __shfl_xor(owner, 32, 64));
+                bool done = owner != q4;
+#pragma unroll
+                for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const bool hit = !done && gm[ub][ib][r] == wm;
+                        gm[ub][ib][r] = hit ? -INFINITY : gm[ub][ib][r];
+                        done = done || hit;
+                    }
+                kth = wm;
+            }
+            if (ok && q4 == 0) a.floor[bu * a.n_splits + split] = kth;
         }
         return;
     }
@@ -1852,7 +1944,7 @@ int launch_f32_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t st
 template <bool MM, int ABL = 0>
 int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream, int dtype = LGX_DTYPE_BF16) {
     const int ksteps = (int)(a.d / 16);
-    if constexpr (ABL == 0 || ABL == kMinMaxOnly) {
+    if constexpr (ABL == 0 || ABL == kMinMaxOnly || ABL == kFloorOnly) {
         if (dtype == LGX_DTYPE_F32) {
             switch (ksteps) {
                 case 4: return launch_f32_lds_kernel<4, MM, ABL>(a, p, stream);
@@ -1865,7 +1957,7 @@ int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream, int d
             }
         }
     }
-    if constexpr (ABL != 0 && ABL != kMinMaxOnly) {  // development ablations: d = 256 only
+    if constexpr (ABL != 0 && ABL != kMinMaxOnly && ABL != kFloorOnly) {  // development ablations: d = 256 only
         if (ksteps != 16) {
             set_error("lgx_score_topk: ablation builds exist for d=256 only");
             return LGX_ERR_UNSUPPORTED;
@@ -1903,7 +1995,11 @@ size_t range_list_bytes(const UserRange& r, int k) { return align_up((size_t)(r.
 size_t range_susp_bytes(const UserRange& r) {
     return r.p.lds && r.p.n_splits == 1 ? align_up((size_t)(r.u1 - r.u0) * 2 * kSuspSlots * 8) : 0;
 }
-size_t range_ws_bytes(const UserRange& r, int k) { return 2 * range_list_bytes(r, k) + range_susp_bytes(r); }
+// the LDS kernel's score floors [users, n_splits]
+size_t range_floor_bytes(const UserRange& r) { return r.p.lds ? align_up((size_t)(r.u1 - r.u0) * r.p.n_splits * 4) : 0; }
+size_t range_ws_bytes(const UserRange& r, int k) {
+    return 2 * range_list_bytes(r, k) + range_susp_bytes(r) + range_floor_bytes(r);
+}
 
 int plan_ranges(int64_t B, int64_t n_items, int dtype, int64_t d, int k, UserRange* r) {
     const SplitPlan p = plan_splits(B, n_items, dtype, d, k);
@@ -1937,6 +2033,16 @@ constexpr int64_t kSeedItems = 16384;
 inline bool seeded_sweep(const SplitPlan& p, bool minmax, int64_t n_items) {
     return p.lds && p.n_splits == 1 && !minmax && n_items >= 16 * kSeedItems;
 }
+// Score floors (kFloorOnly): an unseeded LDS sweep -- the first stage of a seeded sweep, or every
+// split of a split launch -- starts its lists at a floor taken from its first kFloorItems items
+// instead of at -inf, which turns the list-filling start (every tile an event for every wave, the
+// exact path throughout) into a filter that passes about k scores per user.  Lab, 131072 users x
+// 1M items, d=256 bf16, masked (profiles/r03_score_lab_stageprof.txt, r03_score_lab_floor.txt): the
+// first stage [0, 16384) 5.10 ms, of which 4.24 ms events; with floors over its first 2048 / 4096 /
+// 8192 / 16384 items (the pass included) 4.26 / 3.78 / 3.30 / 2.87 ms, all 7 stages 57.84 ->
+// 54.40 ms at 16384, lists identical.  Splits shorter than 4 x kFloorItems go without.
+constexpr int64_t kFloorItems = 16384;
+inline bool floored(const SplitPlan& p, bool minmax) { return p.lds && !minmax && p.split_items >= 4 * kFloorItems; }
 
 size_t topk_ws_bytes(int64_t B, int64_t n_items, int k, int dtype, int64_t d) {
     UserRange r[2];
@@ -2034,6 +2140,12 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
                     reinterpret_cast<float*>(wsr), reinterpret_cast<int32_t*>(wsr + list_bytes), minmax,
                     range_susp_bytes(R) ? reinterpret_cast<uint64_t*>(wsr + 2 * list_bytes) : nullptr};
         int rc;
+        if (floored(p, mm)) {  // the floors of every split's first kFloorItems items, then the sweep reads them
+            a.floor = reinterpret_cast<float*>(wsr + 2 * list_bytes + range_susp_bytes(R));
+            a.floor_items = kFloorItems;
+            rc = launch_lds<false, kFloorOnly>(a, p, stream, dtype);
+            if (rc) return rc;
+        }
 #ifdef LGX_DEV_SWITCHES
         ScoreArgs ka = a;
         if (ablate4) ka.mask_indptr = nullptr;
@@ -2050,9 +2162,10 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
                 st.n_items = 3 * hi < 2 * n_items ? hi : n_items;
                 st.seed_items = lo;
                 st.split_items = st.n_items - lo;
-                if (lo > 0) {
+                if (lo > 0) {  // seeded: the floor is for the unseeded first stage only
                     st.seed_score = a.part_score;
                     st.seed_idx = a.part_idx;
+                    st.floor = nullptr;
                 }
                 rc = launch_lds<false>(st, p, stream, dtype);
                 if (st.n_items == n_items) break;

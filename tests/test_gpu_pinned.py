@@ -17,6 +17,8 @@ Tolerances as tests/test_gpu_parity.py: fp32 |gpu - oracle| <= 1e-5 |oracle| + 1
 bf16 storage <= 2e-2 |oracle| + 2e-2 rms(oracle); top-k: k distinct unmasked items, each within
 1e-5 of the exact k-th best (reference: model.py:163-176, Procedure.py:127-135).
 """
+import re
+
 import numpy as np
 import pytest
 import torch
@@ -201,6 +203,62 @@ def test_seeded_full_sweep_equals_one_sweep():
     got = S.gather(1, idx[sel].long())
     assert torch.isfinite(got).all(), "a masked item was returned"
     assert (got >= kth - 1e-5 * kth.abs().clamp(min=1.0)).all()
+
+
+@pytest.mark.parametrize("mode,dtype", [("full-sweep", torch.bfloat16), ("split", torch.bfloat16),
+                                        ("full-sweep", torch.float32), ("split", torch.float32)])
+def test_score_floors_with_ties_and_masked_group_maxima(mode, dtype):
+    """Score floors (kFloorOnly): every unseeded LDS sweep -- the first seeded stage, or each split
+    of a split launch -- starts its lists at the k-th largest of 64 group maxima over its first
+    16384 items, groups holding a masked item dropped.  The catalog repeats 4096 distinct rows at
+    random positions, so a user's best scores come in exact ties spread over many groups; the mask
+    takes out every copy of the user's best row inside each floor window (so the floor must drop
+    those groups) plus random items.  Lists equal, as sets with their values, the unfloored
+    one-launch sweep (the min/max variant runs without floors and seeds)."""
+    d, k = 64, 20
+    if mode == "full-sweep":
+        B, I, wins = 256 * 256, 300_000, [(0, 16384)]
+    else:
+        B, I = 18 * 256, 1_000_000
+    plan = ops.score_topk_plan(B, I, d, dtype, k)
+    if mode == "full-sweep":
+        assert "full-sweep (seeded in stages)" in plan, plan
+    else:
+        ns = int(re.search(r"n_splits=(\d+)", plan).group(1))
+        assert "full-sweep" not in plan and "split" in plan and ns > 1, plan
+        per = -(-(-(-I // 64)) // ns) * 64  # the plan's split_items: whole 64-item tiles per split
+        assert per >= 4 * 16384  # long enough to take floors
+        wins = [(s * per, min(I, s * per + 16384)) for s in range(ns)]
+    g = torch.Generator(device=DEV).manual_seed(61)
+    Q = (torch.randn(B, d, device=DEV, generator=g) / 8).to(dtype)
+    base = (torch.randn(4096, d, device=DEV, generator=g) / 8).to(dtype)
+    rowid = torch.randint(0, 4096, (I,), device=DEV, generator=g)
+    items = base[rowid].contiguous()
+    best = torch.cat([(Q[u0:u0 + 8192].float() @ base.float().T).argmax(1) for u0 in range(0, B, 8192)])
+    parts = [torch.randint(0, I, (B, 30), device=DEV, generator=g)]
+    for lo, hi in wins:  # every copy of the user's best row inside the window
+        order = torch.argsort(rowid[lo:hi])
+        srt = rowid[lo:hi][order]
+        s0 = torch.searchsorted(srt, best)
+        s1 = torch.searchsorted(srt, best, right=True)
+        j = s0[:, None] + torch.arange(int((s1 - s0).max()), device=DEV)[None, :]
+        parts.append(torch.where(j < s1[:, None], lo + order[j.clamp(max=hi - lo - 1)], -1))
+    m = torch.cat(parts, 1).sort(1).values
+    keep = m >= 0
+    keep[:, 1:] &= m[:, 1:] != m[:, :-1]
+    indptr = torch.zeros(B + 1, dtype=torch.int64, device=DEV)
+    indptr[1:] = torch.cumsum(keep.sum(1), 0)
+    mask = (indptr, m[keep].to(torch.int32))
+    idx, val = lgx.score_topk(Q, items, k, mask=mask)
+    idx1, val1, _ = lgx.score_topk(Q, items, k, mask=mask, want_minmax=True)
+    ka, kb = torch.sort(idx.long(), 1), torch.sort(idx1.long(), 1)
+    assert torch.equal(ka.values, kb.values), "floored lists differ from the unfloored sweep"
+    assert torch.equal(val.gather(1, ka.indices), val1.gather(1, kb.indices))
+    assert (idx >= 0).all()
+    # no masked item comes back (keys u * I + item)
+    users = torch.repeat_interleave(torch.arange(B, device=DEV), indptr[1:] - indptr[:-1])
+    got = torch.arange(B, device=DEV)[:, None] * I + idx.long()
+    assert not torch.isin(got, users * I + mask[1].long()).any(), "a masked item was returned"
 
 
 @pytest.mark.parametrize("d,k,rows", [(64, 1, False), (128, 7, True), (128, 32, False), (256, 20, True),

@@ -149,15 +149,41 @@ int main(int argc, char** argv) {
                         j ? ps : nullptr, j ? pi : nullptr, lo};
             st.push_back(x);
         }
+        // LAB_FLOOR=S: the first stage starts from the score floors of items [0, S) (kFloorOnly walk,
+        // timed with the stage and on its own)
+        const int64_t S0 = getenv("LAB_FLOOR") ? std::atoll(getenv("LAB_FLOOR")) : 0;
+        float* fl = nullptr;
+        if (S0 > 0) {
+            HK(hipMalloc(&fl, B * 4));
+            st[0].floor = fl;
+            st[0].floor_items = S0;
+        }
+        auto first = [&](const ScoreArgs& x) -> int {
+            if (S0 > 0 && launch_lds_kernel<16, false, kFloorOnly, 8, 2, false, true, 0, true>(x, q, nullptr)) return 1;
+            return launch<0, 0>(x, q, nullptr);
+        };
+        if (S0 > 0) {
+            float bestfl = 1e30f;
+            for (int r = 0; r < 3; ++r) {
+                float ms;
+                HK(hipEventRecord(e0, nullptr));
+                if (launch_lds_kernel<16, false, kFloorOnly, 8, 2, false, true, 0, true>(st[0], q, nullptr)) return 1;
+                HK(hipEventRecord(e1, nullptr));
+                HK(hipEventSynchronize(e1));
+                HK(hipEventElapsedTime(&ms, e0, e1));
+                bestfl = std::min(bestfl, ms);
+            }
+            std::printf("floor pass over [0, %lld): %.3f ms\n", (long long)S0, bestfl);
+        }
         double tot = 0, totf = 0;
         for (size_t j = 0; j < st.size(); ++j) {
             float best = 1e30f, bestf = 1e30f;
             for (int r = 0; r < 3; ++r) {
                 for (size_t i = 0; i < j; ++i)
-                    if (launch<0, 0>(st[i], q, nullptr)) return 1;
+                    if (i ? launch<0, 0>(st[i], q, nullptr) : first(st[i])) return 1;
                 float ms;
                 HK(hipEventRecord(e0, nullptr));
-                if (launch<0, 0>(st[j], q, nullptr)) return 1;
+                if (j ? launch<0, 0>(st[j], q, nullptr) : first(st[j])) return 1;
                 HK(hipEventRecord(e1, nullptr));
                 HK(hipEventSynchronize(e1));
                 HK(hipEventElapsedTime(&ms, e0, e1));
@@ -179,6 +205,32 @@ int main(int argc, char** argv) {
         }
         std::printf("stages%s: %.2f ms, fast path only %.2f ms (%.0f vs %.0f TF/s)\n", um ? " (unmasked)" : "", tot, totf,
                     2.0 * B * I * d / (tot * 1e-3) / 1e12, 2.0 * B * I * d / (totf * 1e-3) / 1e12);
+        // the chain's lists against a plain one-sweep top-k (as sets per user)
+        for (size_t i = 0; i < st.size(); ++i)
+            if (i ? launch<0, 0>(st[i], q, nullptr) : first(st[i])) return 1;
+        HK(hipDeviceSynchronize());
+        const size_t lk = (size_t)B * k;
+        std::vector<float> a1(lk), a2(lk);
+        std::vector<int32_t> b1(lk), b2(lk);
+        HK(hipMemcpy(a2.data(), ps, lk * 4, hipMemcpyDeviceToHost));
+        HK(hipMemcpy(b2.data(), pi, lk * 4, hipMemcpyDeviceToHost));
+        ScoreArgs one{Q, nullptr, items, B, I, d, um ? nullptr : mp, um ? nullptr : mi, k, 1, I, ps, pi, nullptr, susp};
+        if (launch<0, 0>(one, q, nullptr)) return 1;
+        HK(hipDeviceSynchronize());
+        HK(hipMemcpy(a1.data(), ps, lk * 4, hipMemcpyDeviceToHost));
+        HK(hipMemcpy(b1.data(), pi, lk * 4, hipMemcpyDeviceToHost));
+        int64_t bad = 0;
+        for (int64_t u = 0; u < B; ++u) {
+            std::vector<std::pair<int32_t, float>> x, y;
+            for (int j = 0; j < k; ++j) {
+                x.push_back({b1[u * k + j], a1[u * k + j]});
+                y.push_back({b2[u * k + j], a2[u * k + j]});
+            }
+            std::sort(x.begin(), x.end());
+            std::sort(y.begin(), y.end());
+            if (x != y) ++bad;
+        }
+        std::printf("staged%s vs one sweep: %lld of %lld users differ\n", S0 > 0 ? " (floored)" : "", (long long)bad, (long long)B);
     } else if (getenv("LAB_STAGES")) {  // seeded stages at the given item boundaries (comma list), vs one sweep
         std::vector<int64_t> cut;
         for (const char* c = getenv("LAB_STAGES"); *c;) {
