@@ -566,38 +566,47 @@ struct WaveTopKT {
         LGX_STAT(9, 1);
         const int64_t m0 = need ? a.mask_indptr[b] : 0, m1 = need ? a.mask_indptr[b + 1] : 0;
         const int32_t* mi = a.mask_indices + m0;
-        int32_t lo[kPend], hi[kPend];
+        // the searches run kSearch keys at a time: all kPend at once would hold 5 x kPend registers
+        // live here, which at 12 slots pushes the walk's long-lived state into scratch
+        constexpr int kSearch = kPend < 4 ? kPend : 4;
+        for (int j0 = 0; j0 < kPend; j0 += kSearch) {
+            if (__ballot(((need >> j0) & ((1u << kSearch) - 1u)) != 0u) == 0ull) continue;
+            int32_t lo[kSearch], hi[kSearch], its[kSearch];
 #pragma unroll
-        for (int j = 0; j < kPend; ++j) {
-            lo[j] = 0;
-            hi[j] = (need >> j) & 1u ? (int32_t)(m1 - m0) : 0;
-        }
-        // first index with mi[idx] >= it, for every needed key at once
-        auto searching = [&]() {
-            bool any = false;
+            for (int j = 0; j < kSearch; ++j) {
+                lo[j] = 0;
+                hi[j] = j0 + j < kPend && ((need >> (j0 + j)) & 1u) ? (int32_t)(m1 - m0) : 0;
+                its[j] = 0;
 #pragma unroll
-            for (int j = 0; j < kPend; ++j) any |= lo[j] < hi[j];
-            return (need != 0u) & any;
-        };
-        while (__ballot(searching()) != 0ull) {
-            int32_t v[kPend];
+                for (int q = 0; q < kPend; ++q) its[j] = q == j0 + j ? it[q] : its[j];
+            }
+            // first index with mi[idx] >= it, for every needed key of the batch at once
+            auto searching = [&]() {
+                bool any = false;
 #pragma unroll
-            for (int j = 0; j < kPend; ++j) v[j] = lo[j] < hi[j] ? mi[(lo[j] + hi[j]) >> 1] : 0;
+                for (int j = 0; j < kSearch; ++j) any |= lo[j] < hi[j];
+                return any;
+            };
+            while (__ballot(searching()) != 0ull) {
+                int32_t v[kSearch];
 #pragma unroll
-            for (int j = 0; j < kPend; ++j) {
-                if (lo[j] < hi[j]) {
-                    const int32_t mid = (lo[j] + hi[j]) >> 1;
-                    if (v[j] < it[j]) lo[j] = mid + 1;
-                    else hi[j] = mid;
+                for (int j = 0; j < kSearch; ++j) v[j] = lo[j] < hi[j] ? mi[(lo[j] + hi[j]) >> 1] : 0;
+#pragma unroll
+                for (int j = 0; j < kSearch; ++j) {
+                    if (lo[j] < hi[j]) {
+                        const int32_t mid = (lo[j] + hi[j]) >> 1;
+                        if (v[j] < its[j]) lo[j] = mid + 1;
+                        else hi[j] = mid;
+                    }
                 }
             }
+#pragma unroll
+            for (int j = 0; j < kSearch; ++j) {
+                const bool needed = j0 + j < kPend && ((need >> (j0 + j)) & 1u);
+                const int32_t w = needed && lo[j] < (int32_t)(m1 - m0) ? mi[lo[j]] : -1;
+                if (needed && w == its[j]) keep &= ~(1u << (j0 + j));
+            }
         }
-        int32_t w[kPend];
-#pragma unroll
-        for (int j = 0; j < kPend; ++j) w[j] = ((need >> j) & 1u) && lo[j] < (int32_t)(m1 - m0) ? mi[lo[j]] : -1;
-#pragma unroll
-        for (int j = 0; j < kPend; ++j)
-            if (((need >> j) & 1u) && w[j] == it[j]) keep &= ~(1u << j);
         return keep;
     }
 
@@ -1944,7 +1953,13 @@ int launch_f32_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t st
 template <bool MM, int ABL = 0>
 int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream, int dtype = LGX_DTYPE_BF16) {
     const int ksteps = (int)(a.d / 16);
-    if constexpr (ABL == 0 || ABL == kMinMaxOnly || ABL == kFloorOnly) {
+    if constexpr (ABL == kFloorOnly) {
+        if (dtype == LGX_DTYPE_F32) {
+            set_error("lgx_score_topk: score floors are a bf16 LDS kernel mode");
+            return LGX_ERR_UNSUPPORTED;
+        }
+    }
+    if constexpr (ABL == 0 || ABL == kMinMaxOnly) {
         if (dtype == LGX_DTYPE_F32) {
             switch (ksteps) {
                 case 4: return launch_f32_lds_kernel<4, MM, ABL>(a, p, stream);
@@ -2040,9 +2055,13 @@ inline bool seeded_sweep(const SplitPlan& p, bool minmax, int64_t n_items) {
 // 1M items, d=256 bf16, masked (profiles/r03_score_lab_stageprof.txt, r03_score_lab_floor.txt): the
 // first stage [0, 16384) 5.10 ms, of which 4.24 ms events; with floors over its first 2048 / 4096 /
 // 8192 / 16384 items (the pass included) 4.26 / 3.78 / 3.30 / 2.87 ms, all 7 stages 57.84 ->
-// 54.40 ms at 16384, lists identical.  Splits shorter than 4 x kFloorItems go without.
+// 54.40 ms at 16384, lists identical.  Splits shorter than 4 x kFloorItems go without, and so does
+// fp32: at 1/16 of the bf16 MFMA rate its events are cheap beside its tiles, and the pass cost more
+// than it saved (bench fp32 leg 1044 -> 1052 ms with floors; bf16 leg 432 -> 418 ms).
 constexpr int64_t kFloorItems = 16384;
-inline bool floored(const SplitPlan& p, bool minmax) { return p.lds && !minmax && p.split_items >= 4 * kFloorItems; }
+inline bool floored(const SplitPlan& p, bool minmax, int dtype) {
+    return p.lds && !minmax && dtype == LGX_DTYPE_BF16 && p.split_items >= 4 * kFloorItems;
+}
 
 size_t topk_ws_bytes(int64_t B, int64_t n_items, int k, int dtype, int64_t d) {
     UserRange r[2];
@@ -2140,7 +2159,7 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
                     reinterpret_cast<float*>(wsr), reinterpret_cast<int32_t*>(wsr + list_bytes), minmax,
                     range_susp_bytes(R) ? reinterpret_cast<uint64_t*>(wsr + 2 * list_bytes) : nullptr};
         int rc;
-        if (floored(p, mm)) {  // the floors of every split's first kFloorItems items, then the sweep reads them
+        if (floored(p, mm, dtype)) {  // the floors of every split's first kFloorItems items, then the sweep reads them
             a.floor = reinterpret_cast<float*>(wsr + 2 * list_bytes + range_susp_bytes(R));
             a.floor_items = kFloorItems;
             rc = launch_lds<false, kFloorOnly>(a, p, stream, dtype);

@@ -68,6 +68,52 @@ def test_lgx_csr_struct_layout_matches_header(tmp_path):
     assert got == want
 
 
+# the kernels bench.py times and the f4 label walk: their state stays in registers
+HOT_KERNELS = ("spmm_segments", "spmm_fixup", "score_topk_bf16_lds", "score_topk_f32_lds", "score_topk_finalize",
+               "strat_label_lds", "layer_epilogue")
+
+
+def test_hot_kernels_do_not_spill_to_scratch(tmp_path):
+    """Host only: the hot gfx950 kernels of liblgx.so keep their state in registers -- no VGPR spills
+    and no private (scratch) segment, read from the code object's metadata.  A spill in the scoring
+    walk put a scratch reload on every top-k event (profiles/r03_score_lab_ws.txt: 54.79 -> 52.37 ms).
+    (The fp32 d=256 dense-score walk, score_dense_lds<f32, 32>, spills two 64-bit tile addresses and
+    is not in the list.)"""
+    import re
+    import shutil
+    import subprocess
+    llvm = "/opt/rocm/lib/llvm/bin"
+    if not (shutil.which("objcopy") and os.path.exists(f"{llvm}/clang-offload-bundler")):
+        pytest.skip("objcopy / clang-offload-bundler not available")
+    so = os.path.join(ROOT, "factors_of_serendipity_recommendation_amd", "liblgx.so")
+    fat = tmp_path / "fat.bin"
+    subprocess.check_call(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", so, str(fat)])
+    # one offload bundle per translation unit, concatenated (and aligned) in the section
+    blob = fat.read_bytes()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    starts = [m.start() for m in re.finditer(re.escape(magic), blob)]
+    assert len(starts) >= 5
+    kernels = []
+    for j, st in enumerate(starts):
+        part, co = tmp_path / f"b{j}.bin", tmp_path / f"b{j}.o"
+        part.write_bytes(blob[st:starts[j + 1] if j + 1 < len(starts) else len(blob)])
+        subprocess.check_call([f"{llvm}/clang-offload-bundler", "--type=o",
+                               "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={part}", f"--output={co}",
+                               "--unbundle"])
+        notes = subprocess.check_output([f"{llvm}/llvm-readelf", "--notes", str(co)]).decode()
+        kernels += [b for b in notes.split("- .agpr_count:") if ".name:" in b]
+    assert len(kernels) > 50
+    bad = []
+    for b in kernels:
+        name = re.search(r"\.name:\s+(\S+)", b).group(1)
+        spill = int(re.search(r"\.vgpr_spill_count:\s+(\d+)", b).group(1))
+        priv = int(re.search(r"\.private_segment_fixed_size:\s+(\d+)", b).group(1))
+        if (spill or priv) and any(h in name for h in HOT_KERNELS):
+            bad.append((name, spill, priv))
+    assert sum(any(h in b for h in HOT_KERNELS) for b in kernels) >= 20
+    assert not bad, bad
+
+
 def test_ops_refuse_cpu_tensors():
     import torch
     import factors_of_serendipity_recommendation_amd as lgx

@@ -208,7 +208,8 @@ def test_seeded_full_sweep_equals_one_sweep():
 @pytest.mark.parametrize("mode,dtype", [("full-sweep", torch.bfloat16), ("split", torch.bfloat16),
                                         ("full-sweep", torch.float32), ("split", torch.float32)])
 def test_score_floors_with_ties_and_masked_group_maxima(mode, dtype):
-    """Score floors (kFloorOnly): every unseeded LDS sweep -- the first seeded stage, or each split
+    """Score floors (kFloorOnly, bf16; the fp32 cases pin the unfloored walk on the same data): every
+    unseeded bf16 LDS sweep -- the first seeded stage, or each split
     of a split launch -- starts its lists at the k-th largest of 64 group maxima over its first
     16384 items, groups holding a masked item dropped.  The catalog repeats 4096 distinct rows at
     random positions, so a user's best scores come in exact ties spread over many groups; the mask

@@ -2,6 +2,7 @@
 // d=256, top-20, 50 masked items per user), launched directly (no finalize), hipEvents, best of 3.
 //   make -C tools score_lab && tools/score_lab [B]
 #include "../factors_of_serendipity_recommendation_amd/csrc/score_topk.hip"
+#include "score_lab_ws.h"
 
 #include <cstdio>
 #include <random>
@@ -12,6 +13,26 @@
 template <int ABL, int DMAPOS, bool SKIP = true, bool STAG = true>
 int launch(const ScoreArgs& a, const SplitPlan& p, hipStream_t s) {
     return launch_lds_kernel<16, false, ABL, 8, 2, STAG, true, DMAPOS, SKIP>(a, p, s);
+}
+
+// the wave-specialised walk (score_topk_bf16_ws), d = 256, full sweep
+template <int WSV>
+int launch_ws_v(const ScoreArgs& a, const SplitPlan& p, hipStream_t s) {
+    typedef LdsGeom<16, kWsMfma, 2, 2> G;
+    const int nbuf = 2;
+    const WsLayout L = ws_layout(a.k, (size_t)nbuf * G::TILE);
+    if (L.total > kLdsBytes) { std::printf("ws: %zu B of LDS\n", L.total); return 1; }
+    if (hipFuncSetAttribute((const void*)score_topk_bf16_ws<16, WSV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.total))
+        return 1;
+    score_topk_bf16_ws<16, WSV><<<(unsigned)p.n_utiles, kWsWaves * 64, L.total, s>>>(a, p.n_utiles, nbuf);
+    return hipGetLastError() != hipSuccess;
+}
+int launch_ws(const ScoreArgs& a, const SplitPlan& p, hipStream_t s) {
+    const char* v = getenv("LAB_WS");
+    if (v && v[0] == '1') return launch_ws_v<1>(a, p, s);
+    if (v && v[0] == '2') return launch_ws_v<2>(a, p, s);
+    if (v && v[0] == '3') return launch_ws_v<3>(a, p, s);
+    return launch_ws_v<0>(a, p, s);
 }
 
 int main(int argc, char** argv) {
@@ -158,9 +179,12 @@ int main(int argc, char** argv) {
             st[0].floor = fl;
             st[0].floor_items = S0;
         }
+        // LAB_WS: the stages run the wave-specialised walk
+        const bool wsk = getenv("LAB_WS") != nullptr;
+        auto main_launch = [&](const ScoreArgs& x) { return wsk ? launch_ws(x, q, nullptr) : launch<0, 0>(x, q, nullptr); };
         auto first = [&](const ScoreArgs& x) -> int {
             if (S0 > 0 && launch_lds_kernel<16, false, kFloorOnly, 8, 2, false, true, 0, true>(x, q, nullptr)) return 1;
-            return launch<0, 0>(x, q, nullptr);
+            return main_launch(x);
         };
         if (S0 > 0) {
             float bestfl = 1e30f;
@@ -180,10 +204,10 @@ int main(int argc, char** argv) {
             float best = 1e30f, bestf = 1e30f;
             for (int r = 0; r < 3; ++r) {
                 for (size_t i = 0; i < j; ++i)
-                    if (i ? launch<0, 0>(st[i], q, nullptr) : first(st[i])) return 1;
+                    if (i ? main_launch(st[i]) : first(st[i])) return 1;
                 float ms;
                 HK(hipEventRecord(e0, nullptr));
-                if (j ? launch<0, 0>(st[j], q, nullptr) : first(st[j])) return 1;
+                if (j ? main_launch(st[j]) : first(st[j])) return 1;
                 HK(hipEventRecord(e1, nullptr));
                 HK(hipEventSynchronize(e1));
                 HK(hipEventElapsedTime(&ms, e0, e1));
@@ -207,7 +231,7 @@ int main(int argc, char** argv) {
                     2.0 * B * I * d / (tot * 1e-3) / 1e12, 2.0 * B * I * d / (totf * 1e-3) / 1e12);
         // the chain's lists against a plain one-sweep top-k (as sets per user)
         for (size_t i = 0; i < st.size(); ++i)
-            if (i ? launch<0, 0>(st[i], q, nullptr) : first(st[i])) return 1;
+            if (i ? main_launch(st[i]) : first(st[i])) return 1;
         HK(hipDeviceSynchronize());
         const size_t lk = (size_t)B * k;
         std::vector<float> a1(lk), a2(lk);
@@ -230,7 +254,7 @@ int main(int argc, char** argv) {
             std::sort(y.begin(), y.end());
             if (x != y) ++bad;
         }
-        std::printf("staged%s vs one sweep: %lld of %lld users differ\n", S0 > 0 ? " (floored)" : "", (long long)bad, (long long)B);
+        std::printf("staged%s%s vs one sweep: %lld of %lld users differ\n", S0 > 0 ? " (floored)" : "", wsk ? " (ws)" : "", (long long)bad, (long long)B);
     } else if (getenv("LAB_STAGES")) {  // seeded stages at the given item boundaries (comma list), vs one sweep
         std::vector<int64_t> cut;
         for (const char* c = getenv("LAB_STAGES"); *c;) {
