@@ -995,7 +995,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(ahead, ntiles) - 1));
     __syncthreads();
     int buf = 0, sbuf = ahead;  // buffer of tile t / of tile t + ahead
-    const bool late = STAGGER && LIKE_PRODUCT && wave >= WAVES / 2;  // wave-uniform
+    const bool late = STAGGER && (LIKE_PRODUCT || ABLATE == kFloorOnly) && wave >= WAVES / 2;  // wave-uniform
     f32x16 acc0, acc1;  // late waves: tile t-1's scores, held across the barrier
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     f32x4 c[2][4];      // 16x16x32 accumulators: c[ub][ib] = items 16 ib + 4 (lane >> 4) + reg, user 16 ub + (lane & 15)
@@ -1148,6 +1148,15 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         for (int ib = 0; ib < 4; ++ib) gm[ub][ib] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
     auto floor_tile = [&](int64_t e0) {
         const int64_t rem = i_end - e0;
+        if (rem >= G::TILE_ITEMS) {
+#pragma unroll
+            for (int ub = 0; ub < 2; ++ub)
+#pragma unroll
+                for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) gm[ub][ib][r] = fmaxf(gm[ub][ib][r], c[ub][ib][r]);
+            return;
+        }
 #pragma unroll
         for (int ib = 0; ib < 4; ++ib)
 #pragma unroll

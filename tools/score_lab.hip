@@ -183,7 +183,7 @@ int main(int argc, char** argv) {
         const bool wsk = getenv("LAB_WS") != nullptr;
         auto main_launch = [&](const ScoreArgs& x) { return wsk ? launch_ws(x, q, nullptr) : launch<0, 0>(x, q, nullptr); };
         auto first = [&](const ScoreArgs& x) -> int {
-            if (S0 > 0 && launch_lds_kernel<16, false, kFloorOnly, 8, 2, false, true, 0, true>(x, q, nullptr)) return 1;
+            if (S0 > 0 && launch_lds_kernel<16, false, kFloorOnly, 8, 2, true, true, 0, true>(x, q, nullptr)) return 1;
             return main_launch(x);
         };
         if (S0 > 0) {
@@ -191,7 +191,7 @@ int main(int argc, char** argv) {
             for (int r = 0; r < 3; ++r) {
                 float ms;
                 HK(hipEventRecord(e0, nullptr));
-                if (launch_lds_kernel<16, false, kFloorOnly, 8, 2, false, true, 0, true>(st[0], q, nullptr)) return 1;
+                if (launch_lds_kernel<16, false, kFloorOnly, 8, 2, true, true, 0, true>(st[0], q, nullptr)) return 1;
                 HK(hipEventRecord(e1, nullptr));
                 HK(hipEventSynchronize(e1));
                 HK(hipEventElapsedTime(&ms, e0, e1));
