@@ -3,6 +3,7 @@
 //   make -C tools score_lab && tools/score_lab [B]
 #include "../factors_of_serendipity_recommendation_amd/csrc/score_topk.hip"
 #include "score_lab_ws.h"
+#include "score_lab_w1.h"
 
 #include <cstdio>
 #include <random>
@@ -152,6 +153,43 @@ int main(int argc, char** argv) {
         }
         std::printf("B=%lld + tail %lld (splits %d): stages then tail %.2f ms (tail alone %.2f) | tail beside the stages %.2f ms (%.1f %%)\n",
                     (long long)B, (long long)T, pt.n_splits, seq, tl, conc, 100.0 * (seq - conc) / seq);
+    } else if (getenv("LAB_W1")) {  // one-wave-per-SIMD walk ceiling vs the product walk's fast path, one sweep
+        SplitPlan q = p;
+        q.n_splits = 1;
+        ScoreArgs x{Q, nullptr, items, B, I, d, nullptr, nullptr, k, 1, I, reinterpret_cast<float*>(ws),
+                    reinterpret_cast<int32_t*>(static_cast<char*>(ws) + (size_t)B * k * 4), nullptr, nullptr};
+        unsigned* evd;
+        HK(hipMalloc(&evd, 4));
+        const int64_t ut1 = (B + kW1Waves * kW1Users - 1) / (kW1Waves * kW1Users);
+        const double fl = 2.0 * B * I * d;
+        for (int nb = 2; nb <= 4; ++nb) {
+            const size_t shm = (size_t)nb * 64 * 512;
+            HK(hipFuncSetAttribute((const void*)score_w1_ceiling<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+            float best = 1e30f;
+            for (int r = 0; r < 4; ++r) {
+                HK(hipMemset(evd, 0, 4));
+                float ms;
+                HK(hipEventRecord(e0, nullptr));
+                score_w1_ceiling<16><<<(unsigned)ut1, kW1Waves * 64, shm>>>(x, ut1, nb, INFINITY, evd);
+                HK(hipEventRecord(e1, nullptr));
+                HK(hipEventSynchronize(e1));
+                HK(hipEventElapsedTime(&ms, e0, e1));
+                if (r) best = std::min(best, ms);
+            }
+            std::printf("w1 ceiling nbuf=%d: %.2f ms %.0f TF/s\n", nb, best, fl / (best * 1e-3) / 1e12);
+            std::fflush(stdout);
+        }
+        float best = 1e30f;
+        for (int r = 0; r < 4; ++r) {
+            float ms;
+            HK(hipEventRecord(e0, nullptr));
+            if (launch<9, 0>(x, q, nullptr)) return 1;
+            HK(hipEventRecord(e1, nullptr));
+            HK(hipEventSynchronize(e1));
+            HK(hipEventElapsedTime(&ms, e0, e1));
+            if (r) best = std::min(best, ms);
+        }
+        std::printf("product fast path only (one sweep): %.2f ms %.0f TF/s\n", best, fl / (best * 1e-3) / 1e12);
     } else if (getenv("LAB_STAGEPROF")) {  // the product's seeded stages, each timed after its predecessors ran
         // untimed (so its seed is what the chain hands it), vs the same stage with tau = +inf (fast path only)
         std::vector<int64_t> cut;
