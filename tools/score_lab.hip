@@ -192,8 +192,17 @@ int main(int argc, char** argv) {
         std::printf("product fast path only (one sweep): %.2f ms %.0f TF/s\n", best, fl / (best * 1e-3) / 1e12);
     } else if (getenv("LAB_STAGEPROF")) {  // the product's seeded stages, each timed after its predecessors ran
         // untimed (so its seed is what the chain hands it), vs the same stage with tau = +inf (fast path only)
+        // LAB_CUTS: other stage boundaries (comma list; the catalog's end is appended)
         std::vector<int64_t> cut;
-        for (int64_t hi = 16384; 3 * hi < 2 * I; hi *= 2) cut.push_back(hi);
+        if (getenv("LAB_CUTS")) {
+            for (const char* c = getenv("LAB_CUTS"); *c;) {
+                cut.push_back(std::atoll(c));
+                while (*c && *c != ',') ++c;
+                if (*c) ++c;
+            }
+        } else {
+            for (int64_t hi = 16384; 3 * hi < 2 * I; hi *= 2) cut.push_back(hi);
+        }
         cut.push_back(I);
         const bool um = getenv("LAB_UNMASKED") != nullptr;
         uint64_t* susp = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + (size_t)B * p.n_splits * k * 8);
