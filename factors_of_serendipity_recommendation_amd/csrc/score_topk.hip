@@ -1503,12 +1503,25 @@ __global__ __launch_bounds__(kDenseWaves * 64) void score_dense_kernel(const voi
 // ds_read_b128 from an XOR-swizzled image (slot ^ (row & 15): the 16 rows a lane group reads sit in
 // 16 different 4-bank groups).  Double-buffered: the next tile's loads are in flight during this
 // tile's MFMAs and stores; one barrier per tile, so idle waves (past B) still take part.
+//
+// Occupancy and stores (round 3, tools/dense_lab.hip, profiles/r03_dense_lab*.txt): with <= 16 chunks
+// (bf16; <= 8 for fp32) the kernel is held to 128 VGPRs, i.e. 4 waves per SIMD = two workgroups per CU, so one
+// workgroup's MFMAs and stores run while the other waits for its tile (at 166 VGPRs a CU held one
+// workgroup, whose waves all stall on the same tile load at each barrier).  The 16 score stores of
+// a tile go out as a wave-uniform row base (SGPRs) plus one 32-bit lane byte offset instead of 16
+// live 64-bit addresses, which is what makes 128 VGPRs fit without scratch.  [4096, 1M] d=256
+// bf16: 4.40-4.96 -> 3.41-3.57 ms (same bits), against 2.45-3.01 ms for the bare store pattern.
+// (fp32 rows hold half the features per chunk, and the f32 KCH = 16 walk needs a few more registers
+// for its 4 MFMAs per chunk: 12 B of scratch at 128 VGPRs, so it keeps two waves per SIMD)
+__host__ __device__ constexpr int dense_waves_per_simd(int dt, int kch) {
+    return kch <= (dt == LGX_DTYPE_BF16 ? 16 : 8) ? 4 : 2;
+}
+
 template <int DT, int KCH>
-__global__ __launch_bounds__(kDenseWaves * 64) void score_dense_lds(const void* Q, const int64_t* user_rows,
-                                                                     const void* items, int64_t B, int64_t n_items,
-                                                                     int64_t d, int apply_sigmoid,
-                                                                     float* __restrict__ out, int64_t n_ug,
-                                                                     int64_t split_items) {
+__global__ __launch_bounds__(kDenseWaves * 64)
+__attribute__((amdgpu_waves_per_eu(dense_waves_per_simd(DT, KCH), dense_waves_per_simd(DT, KCH))))
+void score_dense_lds(const void* Q, const int64_t* user_rows, const void* items, int64_t B, int64_t n_items,
+                     int64_t d, int apply_sigmoid, float* __restrict__ out, int64_t n_ug, int64_t split_items) {
     static_assert(KCH >= 8, "swizzle needs >= 16 slots per row");
     typedef Frag<DT> F;
     constexpr int SPR = 2 * KCH;           // 16-B slots per item row (a chunk = 32 B = two halves)
@@ -1517,12 +1530,12 @@ __global__ __launch_bounds__(kDenseWaves * 64) void score_dense_lds(const void* 
     constexpr int NL = 32 * SPR / (kDenseWaves * 64);  // slots per thread per tile
     static_assert(NL >= 1 && 32 * SPR % (kDenseWaves * 64) == 0, "tile slots must divide over the workgroup");
     __shared__ __attribute__((aligned(16))) unsigned char img[2][TILE];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5, col = lane & 31;
     const int64_t L = blockIdx.x, kk = L >> 3;
     const int64_t ug = kk % n_ug;
     const int64_t split = (kk / n_ug) * 8 + (L & 7);
-    const int64_t u0 = ug * kDenseUsers + (int64_t)wave * kUsersPerWave;
+    const int64_t u0 = ug * kDenseUsers + (int64_t)wave * kUsersPerWave;  // wave-uniform
     const bool wave_on = u0 < B;
     const int64_t b = u0 + col;
     const bool user_ok = b < B;
@@ -1572,14 +1585,16 @@ __global__ __launch_bounds__(kDenseWaves * 64) void score_dense_lds(const void* 
                 const uint4 fr = *reinterpret_cast<const uint4*>(rowp + (((2 * c + h) ^ (col & 15)) * 16));
                 acc = F::mma(uf[c], __builtin_bit_cast(typename F::chunk, fr), acc);
             }
-            const int64_t item_row = i0 + col;
-            if (item_row < i_end) {
+            if (i0 + col < i_end) {
+                // row base of register r: out + (u0 + tile_row(r, 0)) * n_items + i0 (uniform), lane
+                // offset (4 h rows + col) in bytes (< 2^32: asserted by the host, 4 * n_items * 4 + 128)
+                const uint32_t boff = ((uint32_t)(4 * h) * (uint32_t)n_items + (uint32_t)col) * 4u;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const int64_t u = u0 + tile_row(r, h);
-                    if (u < B) {
+                    if (u0 + tile_row(r, h) < B) {
                         const float sc = acc[r];
-                        out[u * n_items + item_row] = apply_sigmoid ? 1.0f / (1.0f + expf(-sc)) : sc;
+                        char* base = reinterpret_cast<char*>(out + (u0 + tile_row(r, 0)) * n_items + i0);
+                        *reinterpret_cast<float*>(base + boff) = apply_sigmoid ? 1.0f / (1.0f + expf(-sc)) : sc;
                     }
                 }
             }
@@ -2283,6 +2298,8 @@ extern "C" int lgx_score_dense(const void* Q, const int64_t* user_rows, const vo
     const int64_t split_items = 32 * ceil_div(tiles, n_splits);
     const int64_t grid = n_ug * n_splits;
     LGX_REQUIRE(grid < (1LL << 31), LGX_ERR_UNSUPPORTED, "lgx_score_dense: %lld users is too many", (long long)B);
+    LGX_REQUIRE(n_items < (1LL << 27), LGX_ERR_UNSUPPORTED, "lgx_score_dense: %lld items is too many (< 2^27)",
+                (long long)n_items);
 #define LGX_SD(DTV, KC)                                                                                    \
     if constexpr (KC >= 8)                                                                                 \
         score_dense_lds<DTV, KC><<<(unsigned)grid, kDenseWaves * 64, 0, stream>>>(Q, user_rows, items, B,   \

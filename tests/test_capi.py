@@ -70,15 +70,15 @@ def test_lgx_csr_struct_layout_matches_header(tmp_path):
 
 # the kernels bench.py times and the f4 label walk: their state stays in registers
 HOT_KERNELS = ("spmm_segments", "spmm_fixup", "score_topk_bf16_lds", "score_topk_f32_lds", "score_topk_finalize",
-               "strat_label_lds", "layer_epilogue")
+               "strat_label_lds", "layer_epilogue", "score_dense_lds")
 
 
 def test_hot_kernels_do_not_spill_to_scratch(tmp_path):
     """Host only: the hot gfx950 kernels of liblgx.so keep their state in registers -- no VGPR spills
     and no private (scratch) segment, read from the code object's metadata.  A spill in the scoring
     walk put a scratch reload on every top-k event (profiles/r03_score_lab_ws.txt: 54.79 -> 52.37 ms).
-    (The fp32 d=256 dense-score walk, score_dense_lds<f32, 32>, spills two 64-bit tile addresses and
-    is not in the list.)"""
+    The dense-score walk is held to 128 VGPRs where that fits without scratch (dense_waves_per_simd);
+    its stores from a wave-uniform base removed the two spilled tile addresses of the fp32 d=256 walk."""
     import re
     import shutil
     import subprocess
