@@ -1,0 +1,252 @@
+// Development: A/B timing of f4's fused label kernel (strat_label_lds, recommend.py:375-381) on the
+// f4 row's batch: 4096 users x 1M items, d=64 f32, 10 folds; hipEvents, median of 5.
+//   make -C tools strat_lab && tools/strat_lab
+// Variants of the per-user label counts: LDS atomics per score (the product), none (timing only),
+// packed 8-bit counters in registers flushed to LDS every 8 tiles; and the register budget of 3
+// workgroups per CU.  Labels and counts are compared with the product kernel's, bit for bit.
+#include "../factors_of_serendipity_recommendation_amd/csrc/score_topk.hip"
+
+#include <cstdio>
+#include <vector>
+
+#define HK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { std::printf("%s -> %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
+
+namespace lgx {
+namespace {
+
+// strat_label_lds<f32, KCH, VEC4 = true, EST1 = true> with HM: 0 LDS atomics per score, 1 no counts,
+// 2 packed counters (bins 0..15: two u64 of 8-bit fields, flushed every 8 tiles: at most 16 x 8 =
+// 128 increments of a field in between)
+template <int KCH, int HM>
+__device__ __forceinline__ void strat_body(const void* Q, const void* items, int64_t B, int64_t n_items, int64_t d,
+                                           StratThr thr, int8_t* __restrict__ labels, int32_t* __restrict__ hist,
+                                           int64_t n_ug, int64_t split_items) {
+    typedef Frag<LGX_DTYPE_F32> F;
+    constexpr int SPR = 2 * KCH, RB = SPR * 16, TILE = 32 * RB, NL = 32 * SPR / (kDenseWaves * 64);
+    __shared__ __attribute__((aligned(16))) unsigned char img[2][TILE];
+    __shared__ float2 TP[33];
+    __shared__ uint32_t hc[kDenseUsers * kHistStride];
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int h = lane >> 5, col = lane & 31;
+    auto thr_at = [&](int j) { return j == 0 ? -INFINITY : (j <= thr.n ? thr.t[j - 1] : INFINITY); };
+    if (threadIdx.x < 33) TP[threadIdx.x] = make_float2(thr_at(threadIdx.x), thr_at(threadIdx.x + 1));
+    for (int e = threadIdx.x; e < kDenseUsers * kHistStride; e += kDenseWaves * 64) hc[e] = 0u;
+    const int64_t L = blockIdx.x, kk = L >> 3;
+    const int64_t ug = kk % n_ug, split = (kk / n_ug) * 8 + (L & 7);
+    const int64_t u0 = ug * kDenseUsers + (int64_t)wave * kUsersPerWave;
+    const bool wave_on = u0 < B;
+    const int64_t b = u0 + col;
+    const bool user_ok = b < B;
+    typename F::chunk uf[KCH];
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) uf[c] = F::load(Q, user_ok ? b : 0, d, c, h, user_ok);
+    const int64_t i_begin = split * split_items, i_end = std::min(n_items, i_begin + split_items);
+    const int64_t row_bytes = d * 4;
+    const unsigned char* ib = static_cast<const unsigned char*>(items);
+    int8_t* lab = labels + b * n_items;
+    uint4 nx[NL];
+    auto load_tile = [&](int64_t i0) {
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int sl = threadIdx.x + j * kDenseWaves * 64;
+            const int r = sl / SPR, q = sl % SPR;
+            const int64_t it = i0 + r;
+            nx[j] = it < i_end ? *reinterpret_cast<const uint4*>(ib + it * row_bytes + q * 16) : make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
+    auto store_tile = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int sl = threadIdx.x + j * kDenseWaves * 64;
+            const int r = sl / SPR, q = sl % SPR;
+            *reinterpret_cast<uint4*>(&img[buf][r * RB + ((q ^ (r & 15)) * 16)]) = nx[j];
+        }
+    };
+    auto label = [&](float sc) {
+        const float x = (sc - thr.base) * thr.inv;
+        const int l = (x >= (float)thr.n || x != x) ? thr.n : (x < 0.0f ? 0 : (int)x);
+        const float2 tp = TP[l];
+        return (uint32_t)(l - (sc < tp.x && l > 0 ? 1 : 0) + (sc >= tp.y && l < thr.n ? 1 : 0));
+    };
+    uint32_t* hu = hc + (wave * kUsersPerWave + col) * kHistStride;
+    uint64_t plo = 0, phi = 0;
+    auto flush = [&]() {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t c = (uint32_t)(((j < 8 ? plo : phi) >> (8 * (j & 7))) & 255u);
+            if (j <= thr.n && c) atomicAdd(hu + j, c);
+        }
+        plo = phi = 0;
+    };
+    if (i_begin >= i_end) return;
+    load_tile(i_begin);
+    store_tile(0);
+    __syncthreads();
+    int buf = 0, nt = 0;
+    for (int64_t i0 = i_begin; i0 < i_end; i0 += 32) {
+        const bool more = i0 + 32 < i_end;
+        if (more) load_tile(i0 + 32);
+        if (wave_on) {
+            const unsigned char* rowp = &img[buf][col * RB];
+            f32x16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+            for (int c = 0; c < KCH; ++c) {
+                const uint4 fr = *reinterpret_cast<const uint4*>(rowp + (((2 * c + h) ^ (col & 15)) * 16));
+                acc = F::mma(__builtin_bit_cast(typename F::chunk, fr), uf[c], acc);
+            }
+            if (user_ok) {
+                const bool whole = i0 + 32 <= i_end;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int64_t it = i0 + 8 * q + 4 * h;
+                    uint32_t l[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) l[e] = label(acc[4 * q + e]);
+                    const uint32_t w = l[0] | (l[1] << 8) | (l[2] << 16) | (l[3] << 24);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        if (whole || it + e < i_end) {
+                            if (HM == 0) atomicAdd(hu + l[e], 1u);
+                            if (HM == 2) {
+                                const uint64_t one = 1ull << (8 * (l[e] & 7));
+                                plo += l[e] < 8 ? one : 0ull;
+                                phi += l[e] < 8 ? 0ull : one;
+                            }
+                        }
+                    }
+                    if (whole) {
+                        *reinterpret_cast<uint32_t*>(lab + it) = w;
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (it + e < i_end) lab[it + e] = (int8_t)l[e];
+                    }
+                }
+                if (HM == 2 && ++nt == 8) {
+                    nt = 0;
+                    flush();
+                }
+            }
+        }
+        if (more) store_tile(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    if (HM == 2) {
+        if (user_ok) flush();
+        __syncthreads();
+    }
+    if (HM != 1) {
+        const int64_t ub = ug * kDenseUsers;
+        for (int e = threadIdx.x; e < kDenseUsers * kHistStride; e += kDenseWaves * 64) {
+            const int uu = e / kHistStride, l = e % kHistStride;
+            const uint32_t c = hc[e];
+            if (c && l <= thr.n && ub + uu < B) atomicAdd(hist + (ub + uu) * (thr.n + 1) + l, (int32_t)c);
+        }
+    }
+}
+
+template <int KCH, int HM>
+__global__ __launch_bounds__(kDenseWaves * 64) void strat_v(const void* Q, const void* items, int64_t B, int64_t n_items,
+                                                             int64_t d, StratThr thr, int8_t* labels, int32_t* hist,
+                                                             int64_t n_ug, int64_t split_items) {
+    strat_body<KCH, HM>(Q, items, B, n_items, d, thr, labels, hist, n_ug, split_items);
+}
+template <int KCH, int HM>
+__global__ __launch_bounds__(kDenseWaves * 64) __attribute__((amdgpu_waves_per_eu(6, 6)))
+void strat_w6(const void* Q, const void* items, int64_t B, int64_t n_items, int64_t d, StratThr thr, int8_t* labels,
+              int32_t* hist, int64_t n_ug, int64_t split_items) {
+    strat_body<KCH, HM>(Q, items, B, n_items, d, thr, labels, hist, n_ug, split_items);
+}
+
+}  // namespace
+}  // namespace lgx
+
+using namespace lgx;
+
+__global__ void diff8(const int8_t* a, const int8_t* b, int64_t n, unsigned long long* cnt) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    unsigned long long c = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) c += a[i] != b[i];
+    if (c) atomicAdd(cnt, c);
+}
+
+int main() {
+    const int64_t B = 4096, I = 1000000, d = 64;
+    const int nf = 10;
+    void *Q, *items;
+    int8_t *lab, *lref;
+    int32_t *hist, *href;
+    unsigned long long* cnt;
+    HK(hipMalloc(&Q, B * d * 4));
+    HK(hipMalloc(&items, I * d * 4));
+    HK(hipMalloc(&lab, B * I));
+    HK(hipMalloc(&lref, B * I));
+    HK(hipMalloc(&hist, B * (nf + 1) * 4));
+    HK(hipMalloc(&href, B * (nf + 1) * 4));
+    HK(hipMalloc(&cnt, 8));
+    if (lgx_fill_normal(Q, B * d, 0.25f, 1, LGX_DTYPE_F32, nullptr)) return 1;
+    if (lgx_fill_normal(items, I * d, 0.25f, 2, LGX_DTYPE_F32, nullptr)) return 1;
+    // thresholds as lgx_strat_labels_fused derives them (scores ~ N(0, 0.5): min -2.5, fold 0.5)
+    const float min16 = -2.5f, inter16 = 0.5f;
+    StratThr thr{};
+    if (lgx_strat_thresholds(min16, inter16, nf, thr.t)) return 1;
+    thr.n = nf;
+    thr.base = thr.t[0] - (thr.t[nf - 1] - thr.t[0]) / (nf - 1);
+    thr.inv = (float)(nf - 1) / (thr.t[nf - 1] - thr.t[0]);
+    if (!strat_estimate_within_one(thr)) { std::printf("estimate not within one\n"); return 1; }
+    const int64_t n_ug = ceil_div(B, (int64_t)kDenseUsers);
+    const int64_t tiles = ceil_div(I, 32);
+    const int64_t n_splits = std::max<int64_t>(8, std::min(8 * ceil_div(ceil_div(2048, n_ug), 8), 8 * ceil_div(tiles, 8)));
+    const int64_t split_items = 32 * ceil_div(tiles, n_splits);
+    const unsigned grid = (unsigned)(n_ug * n_splits);
+    hipEvent_t e0, e1;
+    HK(hipEventCreate(&e0));
+    HK(hipEventCreate(&e1));
+    const double flops = 2.0 * B * I * d;
+    auto timeit = [&](const char* name, auto&& fn, int check) -> int {
+        std::vector<float> ts;
+        for (int r = 0; r < 6; ++r) {
+            HK(hipMemset(hist, 0, B * (nf + 1) * 4));
+            HK(hipEventRecord(e0, 0));
+            fn();
+            HK(hipEventRecord(e1, 0));
+            HK(hipEventSynchronize(e1));
+            float ms;
+            HK(hipEventElapsedTime(&ms, e0, e1));
+            if (r) ts.push_back(ms);
+        }
+        std::sort(ts.begin(), ts.end());
+        const float ms = ts[ts.size() / 2];
+        std::string verdict;
+        if (check) {
+            unsigned long long nd = 0;
+            HK(hipMemset(cnt, 0, 8));
+            diff8<<<4096, 256>>>(lab, lref, B * I, cnt);
+            HK(hipMemcpy(&nd, cnt, 8, hipMemcpyDeviceToHost));
+            std::vector<int32_t> a(B * (nf + 1)), bb(B * (nf + 1));
+            HK(hipMemcpy(a.data(), hist, a.size() * 4, hipMemcpyDeviceToHost));
+            HK(hipMemcpy(bb.data(), href, bb.size() * 4, hipMemcpyDeviceToHost));
+            verdict = nd ? "labels DIFFER" : "labels same";
+            if (check == 2) verdict += a == bb ? ", counts same" : ", counts DIFFER";
+        }
+        std::printf("%-44s %7.3f ms  %6.1f TF/s  %s\n", name, ms, flops / ms / 1e9, verdict.c_str());
+        std::fflush(stdout);
+        return 0;
+    };
+    // the product kernel (counts from the kernel, before the mask step)
+    timeit("product strat_label_lds<f32, 8, vec4, est1>", [&] {
+        strat_label_lds<LGX_DTYPE_F32, 8, true, true><<<grid, 512>>>(Q, nullptr, items, B, I, d, thr, lref, hist, n_ug, split_items);
+    }, 0);
+    HK(hipMemcpy(href, hist, B * (nf + 1) * 4, hipMemcpyDeviceToDevice));
+    timeit("L0 copy (LDS atomics)", [&] { strat_v<8, 0><<<grid, 512>>>(Q, items, B, I, d, thr, lab, hist, n_ug, split_items); }, 2);
+    timeit("L1 no counts", [&] { strat_v<8, 1><<<grid, 512>>>(Q, items, B, I, d, thr, lab, hist, n_ug, split_items); }, 1);
+    timeit("L2 packed counters", [&] { strat_v<8, 2><<<grid, 512>>>(Q, items, B, I, d, thr, lab, hist, n_ug, split_items); }, 2);
+    timeit("L3 LDS atomics, 6 waves/SIMD", [&] { strat_w6<8, 0><<<grid, 512>>>(Q, items, B, I, d, thr, lab, hist, n_ug, split_items); }, 2);
+    timeit("L4 packed counters, 6 waves/SIMD", [&] { strat_w6<8, 2><<<grid, 512>>>(Q, items, B, I, d, thr, lab, hist, n_ug, split_items); }, 2);
+    timeit("L5 no counts, 6 waves/SIMD", [&] { strat_w6<8, 1><<<grid, 512>>>(Q, items, B, I, d, thr, lab, hist, n_ug, split_items); }, 1);
+    HK(hipDeviceSynchronize());
+    return 0;
+}
