@@ -17,7 +17,7 @@ namespace {
 // strat_label_lds<f32, KCH, VEC4 = true, EST1 = true> with HM: 0 LDS atomics per score, 1 no counts,
 // 2 packed counters (bins 0..15: two u64 of 8-bit fields, flushed every 8 tiles: at most 16 x 8 =
 // 128 increments of a field in between)
-template <int KCH, int HM>
+template <int KCH, int HM, bool TWO = false>
 __device__ __forceinline__ void strat_body(const void* Q, const void* items, int64_t B, int64_t n_items, int64_t d,
                                            StratThr thr, int8_t* __restrict__ labels, int32_t* __restrict__ hist,
                                            int64_t n_ug, int64_t split_items) {
@@ -91,10 +91,32 @@ __device__ __forceinline__ void strat_body(const void* Q, const void* items, int
             f32x16 acc;
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+            if (TWO) {  // timing only: two independent accumulator chains (even / odd chunks), summed
+                f32x16 acc2;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc2[r] = 0.0f;
+#pragma unroll
+                for (int c = 0; c < KCH; c += 2) {
+                    const uint4 f0 = *reinterpret_cast<const uint4*>(rowp + (((2 * c + h) ^ (col & 15)) * 16));
+                    const uint4 f1 = *reinterpret_cast<const uint4*>(rowp + (((2 * c + 2 + h) ^ (col & 15)) * 16));
+                    const float4 a0 = __builtin_bit_cast(float4, f0), a1 = __builtin_bit_cast(float4, f1);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, uf[c].x, acc, 0, 0, 0);
+                    acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, uf[c + 1].x, acc2, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, uf[c].y, acc, 0, 0, 0);
+                    acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, uf[c + 1].y, acc2, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, uf[c].z, acc, 0, 0, 0);
+                    acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.z, uf[c + 1].z, acc2, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, uf[c].w, acc, 0, 0, 0);
+                    acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, uf[c + 1].w, acc2, 0, 0, 0);
+                }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[r] += acc2[r];
+            } else {
 #pragma unroll
             for (int c = 0; c < KCH; ++c) {
                 const uint4 fr = *reinterpret_cast<const uint4*>(rowp + (((2 * c + h) ^ (col & 15)) * 16));
                 acc = F::mma(__builtin_bit_cast(typename F::chunk, fr), uf[c], acc);
+            }
             }
             if (user_ok) {
                 const bool whole = i0 + 32 <= i_end;
@@ -148,11 +170,11 @@ __device__ __forceinline__ void strat_body(const void* Q, const void* items, int
     }
 }
 
-template <int KCH, int HM>
+template <int KCH, int HM, bool TWO = false>
 __global__ __launch_bounds__(kDenseWaves * 64) void strat_v(const void* Q, const void* items, int64_t B, int64_t n_items,
                                                              int64_t d, StratThr thr, int8_t* labels, int32_t* hist,
                                                              int64_t n_ug, int64_t split_items) {
-    strat_body<KCH, HM>(Q, items, B, n_items, d, thr, labels, hist, n_ug, split_items);
+    strat_body<KCH, HM, TWO>(Q, items, B, n_items, d, thr, labels, hist, n_ug, split_items);
 }
 template <int KCH, int HM>
 __global__ __launch_bounds__(kDenseWaves * 64) __attribute__((amdgpu_waves_per_eu(6, 6)))
@@ -247,6 +269,8 @@ int main() {
     timeit("L3 LDS atomics, 6 waves/SIMD", [&] { strat_w6<8, 0><<<grid, 512>>>(Q, items, B, I, d, thr, lab, hist, n_ug, split_items); }, 2);
     timeit("L4 packed counters, 6 waves/SIMD", [&] { strat_w6<8, 2><<<grid, 512>>>(Q, items, B, I, d, thr, lab, hist, n_ug, split_items); }, 2);
     timeit("L5 no counts, 6 waves/SIMD", [&] { strat_w6<8, 1><<<grid, 512>>>(Q, items, B, I, d, thr, lab, hist, n_ug, split_items); }, 1);
+    timeit("L6 no counts, two accumulator chains", [&] { strat_v<8, 1, true><<<grid, 512>>>(Q, items, B, I, d, thr, lab, hist, n_ug, split_items); }, 0);
+    timeit("L7 LDS atomics, two accumulator chains", [&] { strat_v<8, 0, true><<<grid, 512>>>(Q, items, B, I, d, thr, lab, hist, n_ug, split_items); }, 0);
     HK(hipDeviceSynchronize());
     return 0;
 }
