@@ -123,6 +123,19 @@ def test_ops_refuse_cpu_tensors():
         lgx.score_topk(torch.zeros(2, 8), torch.zeros(3, 8), 1)
 
 
+def test_score_dense_rejects_catalogs_past_its_lane_offsets():
+    """lgx_score_dense stores a tile's scores from a wave-uniform row base plus a 32-bit lane byte
+    offset of up to (4 rows x n_items + 31) x 4 B: catalogs of 2^27 items or more are refused before
+    any device work (host only: the pointers are never touched)."""
+    from factors_of_serendipity_recommendation_amd import _lib
+    L = _lib.lib()
+    p = ctypes.c_void_p(16)
+    assert L.lgx_score_dense(p, None, p, 4096, 1 << 27, 256, _lib.LGX_DTYPE_BF16, 0, p, None) == 3
+    assert b"items is too many" in L.lgx_last_error()
+    # empty calls stay no-ops
+    assert L.lgx_score_dense(p, None, p, 0, 1 << 27, 256, _lib.LGX_DTYPE_BF16, 0, p, None) == 0
+
+
 def test_new_entry_points_reject_bad_arguments_before_device_work():
     from factors_of_serendipity_recommendation_amd import _lib
     L = _lib.lib()
