@@ -205,6 +205,7 @@ int lgx_propagate(const lgx_csr* A, const void* E0, float* out, int64_t d, int K
 /* ---------------------------------------------------------------- a6-a9: scoring / top-k */
 /*
  * scores[b, i] = <Q[user_rows ? user_rows[b] : b], items[i]>  (optionally sigmoid), f32 [B, n_items].
+ * n_items < 2^27 (the score stores use 32-bit lane offsets; LGX_ERR_UNSUPPORTED otherwise).
  */
 int lgx_score_dense(const void* Q, const int64_t* user_rows, const void* items, int64_t B,
                     int64_t n_items, int64_t d, int dtype, int apply_sigmoid, float* scores,
