@@ -13,19 +13,28 @@
 namespace lgx {
 namespace {
 
-constexpr int kUnroll = 4;
+constexpr int kUnroll = 3;  // 4 float4 per lane took 77 VGPRs (spills at the 64 of 8 waves per SIMD)
 
 // WPR waves per row (4 for long rows, 1 for short ones: 4 rows per workgroup).  VEC: rows are
 // 16-B aligned, so each lane loads float4s (1 KB per wave instruction).  Per batch of loads one
 // integer compare of ord(score) against the running k-th key's score bits rules out the batch
 // (exact: ties and NaNs go to the merge, which orders by the full key).
 // R: list registers per lane (k <= 64 R, WaveList of wave_topk.h)
+// Occupancy (tools/topk_lab.hip): a long row is 4 MB of reads for one workgroup, so the launch runs in
+// rounds of resident workgroups.  At 77 VGPRs a CU held 6 of them: [4096, 1M] took 2.67 rounds
+// (the last one a third full).  With 3 loads in flight per lane (56 VGPRs, 8 waves per SIMD) a CU
+// holds 8: two full rounds.  A batch's survivors go through one merge (packed in LDS), not one merge
+// per (load, element).  [4096, 1M] k=20: 1.195x -> 1.12x the time of the same reads with no top-k
+// (profiles/r03_topk_lab*.txt).
+__host__ __device__ constexpr int topk_rows_waves_per_simd(int r) { return r == 1 ? 8 : 4; }
+
 template <int WPR, bool VEC, int R>
-__global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict__ S, int64_t rows, int64_t cols,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(topk_rows_waves_per_simd(R), topk_rows_waves_per_simd(R))))
+void topk_rows_kernel(const float* __restrict__ S, int64_t rows, int64_t cols,
                                                         int64_t ld, int k, int32_t* __restrict__ out_idx,
                                                         float* __restrict__ out_val) {
     __shared__ uint64_t lists[4][R][kWave];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int sub = wave % WPR;                       // this wave's part of its row
     const int64_t row = (int64_t)blockIdx.x * (4 / WPR) + wave / WPR;
     if (row >= rows) return;                          // no barrier is reached by a missing row's waves
@@ -36,12 +45,14 @@ __global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict_
     const int64_t stride = (int64_t)kWave * V * WPR;  // columns per wave round
     for (int64_t base = (int64_t)sub * kWave * V; base < cols; base += stride * kUnroll) {
         float v[kUnroll][V];
+        const float* sb = s + base;  // wave-uniform: the loads are a scalar base + a 32-bit lane offset
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
-            const int64_t c0 = base + u * stride + (int64_t)lane * V;
+            const int off = u * (int)stride + lane * V;
+            const int64_t c0 = base + off;
             if (VEC) {
                 if (c0 + 3 < cols) {
-                    const float4 q = *reinterpret_cast<const float4*>(s + c0);
+                    const float4 q = *reinterpret_cast<const float4*>(sb + off);
                     v[u][0] = q.x; v[u][V > 1 ? 1 : 0] = q.y; v[u][V > 2 ? 2 : 0] = q.z; v[u][V > 3 ? 3 : 0] = q.w;
                 } else {
 #pragma unroll
@@ -58,13 +69,41 @@ __global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict_
 #pragma unroll
             for (int j = 0; j < V; ++j) any |= base + u * stride + (int64_t)lane * V + j < cols && ord_f32(v[u][j]) >= thr_hi;
         if (__ballot(any) == 0ull) continue;
+        // survivors of the batch (score bits >= the k-th key's) packed into one 64-lane candidate
+        // vector through this wave's LDS row, so a batch costs one merge instead of one per (u, j);
+        // a batch with more than 64 survivors (a list still filling) merges per (u, j) as before
+        uint64_t* pk = &lists[wave][0][0];
+        int n = 0;
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u)
 #pragma unroll
             for (int j = 0; j < V; ++j) {
                 const int64_t c = base + u * stride + (int64_t)lane * V + j;
-                top.push(c < cols ? make_key(v[u][j], (int32_t)c) : 0ull, k, lane);
+                const bool pass = c < cols && ord_f32(v[u][j]) >= thr_hi;
+                const uint64_t m = __ballot(pass);
+                const int pos = n + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                if (pass && pos < kWave) pk[pos] = make_key(v[u][j], (int32_t)c);
+                n += __popcll(m);
             }
+        if (n <= kWave) {
+            __builtin_amdgcn_wave_barrier();
+            const uint64_t cand = lane < n ? pk[lane] : 0ull;
+            __builtin_amdgcn_wave_barrier();
+            top.push(cand, k, lane);
+            continue;
+        }
+        // one merge instance in a rolled loop (the value picked by a select chain, so v stays in
+        // registers): twelve inlined merges cost the registers of the 8-waves-per-SIMD budget
+#pragma unroll 1
+        for (int t = 0; t < kUnroll * V; ++t) {
+            float x = v[0][0];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u)
+#pragma unroll
+                for (int j = 0; j < V; ++j) x = t == u * V + j ? v[u][j] : x;
+            const int64_t c = base + (t / V) * stride + (int64_t)lane * V + t % V;
+            top.push(c < cols ? make_key(x, (int32_t)c) : 0ull, k, lane);
+        }
     }
     if (WPR > 1) {
 #pragma unroll

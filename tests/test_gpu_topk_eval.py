@@ -52,6 +52,27 @@ def test_topk_rows_large_k_bit_exact(k, cols):
     assert np.array_equal(val.cpu().numpy(), oval)
 
 
+@pytest.mark.parametrize("k", [1, 20, 64])
+@pytest.mark.parametrize("cols", [5000, 100_000, 100_003])
+def test_topk_rows_batched_survivors_bit_exact(k, cols):
+    """k <= 64: a batch's survivors are packed into one 64-lane merge; a batch with more than 64
+    survivors (ascending rows: every value beats the running k-th) merges value by value.  Short
+    and long rows, float4 and scalar loads, ties and infinities, bit-exact against the oracle."""
+    rng = np.random.default_rng(3 * k + cols)
+    S = rng.standard_normal((24, cols)).astype(np.float32)
+    S[1] = np.arange(cols, dtype=np.float32)            # ascending: every batch overflows 64
+    S[2] = -np.arange(cols, dtype=np.float32)           # descending: no event after the first batch
+    S[3] = 0.25                                         # all ties -> lowest indices
+    S[4, ::97] = 7.0                                    # spread ties above everything else
+    S[5, cols // 2:] = np.inf                           # infinities
+    S[6] = -np.inf
+    S[7, -70:] = 50.0                                   # the best values in the last batch
+    idx, val = lgx.topk_rows(torch.from_numpy(S).to(DEV), k)
+    oidx, oval = oracle.topk_rows(S, k)
+    assert np.array_equal(idx.cpu().numpy(), oidx)
+    assert np.array_equal(val.cpu().numpy(), oval)
+
+
 @pytest.mark.parametrize("dtype,d", [(torch.float32, 64), (torch.bfloat16, 128), (torch.bfloat16, 256)])
 @pytest.mark.parametrize("k", [65, 100, 200])
 def test_score_topk_large_k_masked(dtype, d, k):
