@@ -132,6 +132,29 @@ __device__ __forceinline__ bool in_list(const int32_t* t, int64_t n, int32_t x) 
     return false;
 }
 
+// a user's truth list in registers when it has at most kTruthRegs items: the hit test of a rank is
+// then kTruthRegs compares instead of a chain of dependent global loads (which bounded the kernel:
+// ~200 loads per user at k = 20 and 10 truths)
+constexpr int kTruthRegs = 16;
+struct TruthRegs {
+    int32_t t[kTruthRegs];
+    int64_t n;
+    const int32_t* g;  // the list in global memory (used when n > kTruthRegs)
+    __device__ __forceinline__ void load(const int32_t* truth, int64_t tl) {
+        n = tl;
+        g = truth;
+#pragma unroll
+        for (int j = 0; j < kTruthRegs; ++j) t[j] = j < tl ? truth[j] : 0;
+    }
+    __device__ __forceinline__ bool has(int32_t x) const {
+        if (n > kTruthRegs) return in_list(g, n, x);
+        bool h = false;
+#pragma unroll
+        for (int j = 0; j < kTruthRegs; ++j) h |= j < n && t[j] == x;
+        return h;
+    }
+};
+
 // evaluate_foldout.h:16-112 per user; float accumulators with double increments as in the C++.
 // out[c * ostride + i] for curve c (precision, recall, map, ndcg, mrr) at rank i.
 __device__ __forceinline__ void foldout_user(const int32_t* rank, const int32_t* truth, int64_t tl, int k,
@@ -139,8 +162,10 @@ __device__ __forceinline__ void foldout_user(const int32_t* rank, const int32_t*
     int hits = 0;
     float sum_pre = 0.0f, dcg = 0.0f, idcg = 0.0f;
     bool found = false;
+    TruthRegs tr;
+    tr.load(truth, tl);
     for (int i = 0; i < k; ++i) {
-        const bool hit = in_list(truth, tl, rank[i]);
+        const bool hit = tr.has(rank[i]);
         if (hit) {
             hits += 1;
             const float pre = (float)(1.0 * hits / (i + 1));
