@@ -273,6 +273,99 @@ void dense2(const void* Q, const void* items, int64_t B, int64_t n_items, float*
             int64_t split_items) {
     dense2_body<WV, PF, ABL>(Q, items, B, n_items, out, n_ug, split_items);
 }
+// third round: the tile ring filled by LDS-DMA (global_load_lds_dwordx4, no VGPR staging), NBUF
+// buffers with NBUF-1 tiles in flight.  vmcnt counts the score stores as well as the DMA (gfx9
+// counts both, in order), so the wait for tile t+1 allows this iteration's own DMA pieces plus its
+// 16 stores -- only when the wave issued exactly 16 (a full wave on a whole tile), else vmcnt(0).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void dma16(const void* sbase, uint32_t voff, uint32_t lds_addr) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+                 :: "v"(voff), "s"(sbase), "s"(lds_addr) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+template <int NBUF>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void dense_dma(const void* Q, const void* items, int64_t B, int64_t n_items, float* __restrict__ out, int64_t n_ug,
+               int64_t split_items) {
+    constexpr int KCH = 16, RB = 512, TILE = 32 * RB, PPW = TILE / 1024 / kWaves;  // 2 pieces per wave
+    extern __shared__ __attribute__((aligned(16))) unsigned char ring[];
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int h = lane >> 5, col = lane & 31;
+    const int64_t L = blockIdx.x, kk = L >> 3;
+    const int64_t ug = kk % n_ug, split = (kk / n_ug) * 8 + (L & 7);
+    const int64_t u0 = ug * kUsers + (int64_t)wave * kUPW;
+    const bool wave_on = u0 < B, full_wave = u0 + kUPW <= B;
+    const int64_t b = u0 + col;
+    const bool user_ok = b < B;
+    uint4 uf[KCH];
+#pragma unroll
+    for (int c = 0; c < KCH; ++c)
+        uf[c] = user_ok ? *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(Q) + b * 256 + c * 16 + 8 * h)
+                        : make_uint4(0u, 0u, 0u, 0u);
+    const int64_t i_begin = split * split_items, i_end = std::min(n_items, i_begin + split_items);
+    if (i_begin >= i_end) return;
+    const int64_t ntiles = (i_end - i_begin + 31) / 32;
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)ring;
+    const unsigned char* ib = static_cast<const unsigned char*>(items);
+    auto stage = [&](int buf, int64_t t) {
+        const int64_t t0 = i_begin + t * 32;
+        const uint64_t bu = reinterpret_cast<uint64_t>(ib + t0 * RB);
+        const unsigned char* base = reinterpret_cast<const unsigned char*>(
+            ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(bu >> 32)) << 32) |
+            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)bu));
+        const int last = (int)(i_end - 1 - t0);
+#pragma unroll
+        for (int p = 0; p < PPW; ++p) {
+            const int q = (wave * PPW + p) * 64 + lane;   // LDS slot: row q / 32, chunk q % 32
+            const int row = q / 32, src = (q % 32) ^ (row & 15);
+            const int srow = row > last ? last : row;
+            dma16(base, (uint32_t)(srow * RB + src * 16),
+                  __builtin_amdgcn_readfirstlane(lds0 + buf * TILE + (wave * PPW + p) * 1024));
+        }
+    };
+    const uint32_t boff = (uint32_t)(4 * h * n_items + col) * 4u;
+    for (int j = 0; j < NBUF - 1 && j < ntiles; ++j) stage(j, j);
+    if (ntiles > 1 && NBUF > 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int buf = 0, sbuf = NBUF - 1;
+    for (int64_t t = 0; t < ntiles; ++t) {
+        const int64_t i0 = i_begin + t * 32;
+        const bool refill = t + NBUF - 1 < ntiles;
+        if (refill) stage(sbuf, t + NBUF - 1);
+        int nst = 0;
+        if (wave_on) {
+            const unsigned char* rowp = ring + buf * TILE + col * RB;
+            f32x16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+            for (int c = 0; c < KCH; ++c) {
+                const uint4 fr = *reinterpret_cast<const uint4*>(rowp + (((2 * c + h) ^ (col & 15)) * 16));
+                acc = mma(uf[c], fr, acc);
+            }
+            if (i0 + col < i_end) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const char* base = reinterpret_cast<const char*>(out + (u0 + tile_row(r, 0)) * n_items + i0);
+                    if (u0 + tile_row(r, h) < B) *reinterpret_cast<float*>(const_cast<char*>(base) + boff) = acc[r];
+                }
+            }
+            nst = full_wave && i0 + 32 <= i_end ? 16 : -1;
+        }
+        // tile t+1 must have landed: allow the pieces issued this iteration (+ its 16 stores)
+        if (t + 1 < ntiles) {
+            if (refill && nst == 16) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+            else if (refill && !wave_on) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        buf = buf + 1 == NBUF ? 0 : buf + 1;
+        sbuf = sbuf + 1 == NBUF ? 0 : sbuf + 1;
+    }
+}
 }  // namespace
 
 using lgx::ceil_div;
@@ -363,6 +456,10 @@ int main(int argc, char** argv) {
     timeit("Z3 4 waves, PF2, 4/SIMD", [&] { dense2<4, 2, 0, 4><<<grid4, 256>>>(Q, items, B, I, out, n_ug4, sp4); }, true);
     timeit("Z2a 4 waves, PF1, L2-resident loads", [&] { dense2<4, 1, 3, 4><<<grid4, 256>>>(Q, items, B, I, out, n_ug4, sp4); }, false);
     timeit("Z4 8 waves, PF1, 3/SIMD", [&] { dense2<8, 1, 0, 3><<<grid, 512>>>(Q, items, B, I, out, n_ug, split32); }, true);
+    HK(hipFuncSetAttribute((const void*)dense_dma<3>, hipFuncAttributeMaxDynamicSharedMemorySize, 3 * 32 * 512));
+    HK(hipFuncSetAttribute((const void*)dense_dma<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 32 * 512));
+    timeit("D3 LDS-DMA ring, 3 buffers", [&] { dense_dma<3><<<grid, 512, 3 * 32 * 512>>>(Q, items, B, I, out, n_ug, split32); }, true);
+    timeit("D4 LDS-DMA ring, 4 buffers", [&] { dense_dma<4><<<grid, 512, 4 * 32 * 512>>>(Q, items, B, I, out, n_ug, split32); }, true);
     HK(hipDeviceSynchronize());
     return 0;
 }
