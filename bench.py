@@ -241,8 +241,10 @@ def make_step(A, E0, K, d, dtype, world, cfg, rank, timings):
 
     def step(record):
         step.record = record
+        prop.record_phases = record  # per-phase stamps on the compute stream (distributed.PhaseRecorder)
         prop.step()
     step.record = False
+    step.prop = prop
     return step, shard.A_pull.nnz + shard.A_push.nnz, shard.n_u_local + shard.n_i_local
 
 
@@ -295,11 +297,23 @@ def bench_propagation(args, rank, world, A, cfg, dtype, steps, warmup):
             "traffic_unit": "GB/launch", "traffic_source": tsrc,
             "traffic_rate_gbs": traffic / mean_launch_s if traffic else None,
             "traffic_frac": traffic * 1e9 / mean_launch_s / HBM_PEAK if traffic else None}
+    out = {"dtype": dname, "value": K * nnz_all * steps / elapsed, "unit": "edges/s",
+           "ms_per_step": elapsed / steps * 1e3, "steps": steps, "warmup": warmup, "nnz": nnz_all,
+           "roofline": roof, "E0": E0 if world == 1 else None}
     if world == 1:
         roof["calibration"] = calibration()
-    return {"dtype": dname, "value": K * nnz_all * steps / elapsed, "unit": "edges/s",
-            "ms_per_step": elapsed / steps * 1e3, "steps": steps, "warmup": warmup, "nnz": nnz_all,
-            "roofline": roof, "E0": E0 if world == 1 else None}
+    else:
+        # where a step's time goes on each rank's compute stream, max over ranks per phase: push /
+        # pull / reduce / epilogue are kernels, allgather_wait / exchange_wait the time the stream
+        # sat behind a collective (the communication the schedule left exposed)
+        ph = step.prop.phase_summary()
+        names = ["push", "allgather_wait", "pull", "exchange_wait", "reduce", "epilogue", "comm_exposed_ms"]
+        mx = {n: max_over_ranks(float(ph.get(n, 0.0)), world) for n in names}
+        out["comm_exposed_ms"] = mx.pop("comm_exposed_ms")
+        out["phases_ms"] = mx
+        out["phases_note"] = (f"ms per step on the compute stream, max over {world} ranks; push in "
+                              f"{len(step.prop.push_chunks)} chunks, each exchanged by its own all-to-all")
+    return out
 
 
 # ------------------------------------------------------------------------------------ CPU baseline
@@ -518,6 +532,8 @@ def main():
         "process_group": ({"world_size": dist.get_world_size(), "backend": dist.get_backend()} if world > 1
                           else None),
         "roofline": res["roofline"], "cpu_baseline": cpu,
+        **({"phases_ms": res["phases_ms"], "comm_exposed_ms": res["comm_exposed_ms"],
+            "phases_note": res["phases_note"]} if world > 1 else {}),
         ("bf16" if extra and extra["dtype"] == "bf16" else "fp32"): extra,
         "scoring": scoring, "scoring_bf16": scoring16,
     }

@@ -96,6 +96,7 @@ SIGNATURES = {
                                    ctypes.c_double, _vp, _vp]),
     "lgx_list_dot_reduce": (_c_int, [_vp, _c_i64, _c_int, _c_i64, _vp, _vp, _vp, _vp, _c_int, _vp, _vp]),
     "lgx_layer_epilogue": (_c_int, [_vp, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_float, _vp]),
+    "lgx_sum_slabs": (_c_int, [_vp, _c_i64, _c_i64, _vp, _vp]),
     "lgx_propagate_workspace": (_c_int, [_c_i64, _c_i64, _c_int, _sz_p]),
     "lgx_propagate": (_c_int, [ctypes.POINTER(LgxCSR), _vp, _vp, _c_i64, _c_int, _c_int, _vp, ctypes.c_size_t, _vp]),
     "lgx_score_dense": (_c_int, [_vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _vp, _vp]),

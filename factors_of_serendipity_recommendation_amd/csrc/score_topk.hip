@@ -34,25 +34,6 @@
 namespace lgx {
 namespace {
 
-// Development statistics (tools/score_stats.hip defines LGX_SCORE_STATS; the library never does):
-// per-wave counters and s_memtime cycle stamps, summed into a device array at the end.
-#ifdef LGX_SCORE_STATS
-__device__ unsigned long long g_score_stats[24];
-#define LGX_STAT_DECL uint64_t stat_[24] = {};
-#define LGX_STAT(i, v) (stat_[i] += (v))
-#define LGX_STAT_T0 const uint64_t stat_t0_ = __builtin_amdgcn_s_memtime();
-#define LGX_STAT_T1(i) LGX_STAT(i, __builtin_amdgcn_s_memtime() - stat_t0_);
-#define LGX_STAT_FLUSH                                                                                 \
-    if ((threadIdx.x & 63) == 0)                                                                       \
-        for (int i_ = 0; i_ < 24; ++i_) atomicAdd(&g_score_stats[i_], (unsigned long long)stat_[i_]);
-#else
-#define LGX_STAT_DECL
-#define LGX_STAT(i, v)
-#define LGX_STAT_T0
-#define LGX_STAT_T1(i)
-#define LGX_STAT_FLUSH
-#endif
-
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -132,11 +113,8 @@ struct ScoreArgs {
 // completes in order), and the per-tile barrier makes every wave of the workgroup wait for it.  A
 // lane with all its slots taken searches at once, as before.
 constexpr int kSuspSlots = 24;
-#ifndef LGX_BLOOM_WORDS
-#define LGX_BLOOM_WORDS 8
-#endif
-constexpr int kBloomWords = LGX_BLOOM_WORDS;  // 256-bit filter: 8 VGPRs
-constexpr int kBloomShift = 32 - 5 - (kBloomWords == 16 ? 4 : kBloomWords == 8 ? 3 : 2);
+constexpr int kBloomWords = 8;  // 256-bit filter: 8 VGPRs
+constexpr int kBloomShift = 32 - 5 - 3;
 
 __device__ __forceinline__ bool is_masked(const ScoreArgs& a, int64_t b, int32_t item) {
     if (!a.mask_indptr) return false;
@@ -165,10 +143,7 @@ constexpr int kListSpare = 8;  // the 8-key rescan of user 31 may read past its 
 // 57.75 ms, 1103 (1168 unmasked, +4 %).  12 slots take the LDS of the third ring buffer (the
 // ring's depth measured neutral) and fit d = 256 up to k = 20.
 constexpr int kPendSlots = 4;
-#ifndef LGX_PEND_SLOTS_LDS
-#define LGX_PEND_SLOTS_LDS 12
-#endif
-constexpr int kPendBf16Lds = LGX_PEND_SLOTS_LDS;
+constexpr int kPendBf16Lds = 12;
 __host__ __device__ constexpr size_t list_keys_per_wave(int k) { return (size_t)kUsersPerWave * kstride(k) + kListSpare; }
 // ... then one int per lane: the count of its parked keys (kSuspSlots)
 __host__ __device__ constexpr size_t list_bytes_per_wave(int k, int pend = kPendSlots) {
@@ -199,7 +174,6 @@ struct WaveTopKT {
     // that a late-sweep survivor costs a few register moves instead of LDS round trips
     static constexpr int kPend = PEND;
     static_assert(kPend >= 1 && kPend <= 16, "deferred slots: 1..16 per lane");
-    LGX_STAT_DECL
     // this lane's kPend (+1 scratch) slots in LDS; a slot holds the raw pair (score bits, item << 32)
     uint64_t* pend;
     int pcnt;
@@ -232,33 +206,16 @@ struct WaveTopKT {
     __device__ __forceinline__ bool masked(const ScoreArgs& a, uint64_t key) {
         const int32_t it = key_index(key);
         if (!a.mask_indptr) return false;
-#if defined(LGX_MASK_ABL) && LGX_MASK_ABL == 1  // development (tools/score_lab): no mask test at all
-        return false;
-#endif
-        LGX_STAT(8, 1);
         if (!bloom_test(bloom_h1(it)) || !bloom_test(bloom_h2(it))) return false;
-#if defined(LGX_MASK_ABL) && LGX_MASK_ABL == 2  // development: Bloom filter only, no exact search
-        return false;
-#endif
         if (park) {
             const int c = *scnt();
             if (c < kSuspSlots) {
-#if !defined(LGX_MASK_ABL) || LGX_MASK_ABL != 3  // 3 (development): parking without the store
                 susp_slots(a)[c] = key;
-#endif
                 *scnt() = c + 1;
                 return true;
             }
         }
-        LGX_STAT(9, 1);
-#ifdef LGX_SCORE_STATS
-        const uint64_t t0_ = __builtin_amdgcn_s_memtime();
-        const bool r_ = is_masked(a, b, it);
-        stat_[10] += __builtin_amdgcn_s_memtime() - t0_;
-        return r_;
-#else
         return is_masked(a, b, it);
-#endif
     }
     __device__ __forceinline__ void build_bloom(const ScoreArgs& a) {
 #pragma unroll
@@ -324,10 +281,6 @@ struct WaveTopKT {
 
     // new worst entry: 8 keys (four 16-byte reads issued together) per LDS round trip
     __device__ __forceinline__ void rescan() {
-        LGX_STAT(19, 1);
-#ifdef LGX_SCORE_STATS
-        const uint64_t rs_t0_ = __builtin_amdgcn_s_memtime();
-#endif
         uint64_t m = ~0ull;
         int p = 0;
         for (int j0 = 0; j0 < k; j0 += 8) {
@@ -349,9 +302,6 @@ struct WaveTopKT {
         }
         mp = p;
         kmin = m;
-#ifdef LGX_SCORE_STATS
-        stat_[20] += __builtin_amdgcn_s_memtime() - rs_t0_;
-#endif
     }
 
     // consume NACC (1 or 2) 32-item accumulator tiles; tile j's item rows start at i0 + 32 j
@@ -362,7 +312,7 @@ struct WaveTopKT {
     // 32x32x16 accumulator layout, items 32 j + (r & 3) + 8 (r >> 2) + 4 h
     // TAIL: the block may run past i_end (callers that know it does not pass false, so that the
     // common path never rewrites the accumulators and the compiler keeps them where they are)
-    template <bool MINMAX, int NACC, bool FASTONLY = false, bool L16 = false, bool TAIL = true>
+    template <bool MINMAX, int NACC, bool L16 = false, bool TAIL = true>
     __device__ __forceinline__ void block(const ScoreArgs& a, f32x16 acc0, f32x16 acc1, int64_t i0, int64_t i_end) {
         const int64_t ib = i0 + (L16 ? 8 : 4) * h;  // item of accumulator row 0 of this lane half
         const bool tail = TAIL && i0 + 32 * NACC > i_end;
@@ -397,24 +347,13 @@ struct WaveTopKT {
             mn = fminf(mn, lo);
             mx = fmaxf(mx, m);
         }
-        if (FASTONLY) {  // development ablation: filter only
-            mn = fminf(mn, __ballot(m >= tau) ? 1.0f : 0.0f);
-            return;
-        }
         if (__ballot(m >= tau) == 0ull) return;  // wave-uniform fast path
-        LGX_STAT(1, 1);
-#ifdef LGX_SCORE_STATS
-        const uint64_t ev_t0 = __builtin_amdgcn_s_memtime();
-#endif
         // the wave with an event is the one the workgroup barrier waits for: its VALU work goes
         // ahead of the partner's issue (+1.3 % at the C5 probe; static priority per wave half
         // measured no change)
         __builtin_amdgcn_s_setprio(2);
         slow<NACC, L16>(a, acc0, acc1, g, ib, rem);
         __builtin_amdgcn_s_setprio(0);
-#ifdef LGX_SCORE_STATS
-        stat_[7] += __builtin_amdgcn_s_memtime() - ev_t0;
-#endif
     }
 
     template <bool L16 = false>
@@ -459,19 +398,10 @@ struct WaveTopKT {
                 pcnt = n;
                 return;
             }
-            LGX_STAT(2, 1);
         } else {
-            LGX_STAT(17, 1);
         }
-#ifdef LGX_SCORE_STATS
-        const uint64_t ex_t0_ = __builtin_amdgcn_s_memtime();
-#endif
         drain(a);
         insert_now<NACC, L16>(a, acc0, acc1, ib, survivors<NACC, L16>(acc0, acc1, ib, rem));
-#ifdef LGX_SCORE_STATS
-        stat_[15] += __builtin_amdgcn_s_memtime() - ex_t0_;
-        stat_[16] += 1;
-#endif
     }
 
     template <bool L16>
@@ -534,9 +464,6 @@ struct WaveTopKT {
     __device__ __forceinline__ uint32_t drop_masked(const ScoreArgs& a) {
         uint32_t keep = (1u << pcnt) - 1u;
         if (!a.mask_indptr) return keep;
-#if defined(LGX_MASK_ABL) && LGX_MASK_ABL == 1
-        return keep;
-#endif
         int32_t it[kPend];
         uint32_t need = 0;
 #pragma unroll
@@ -545,16 +472,11 @@ struct WaveTopKT {
             if (j < pcnt && bloom_test(bloom_h1(it[j])) && bloom_test(bloom_h2(it[j]))) need |= 1u << j;
         }
         if (__ballot(need != 0u) == 0ull) return keep;
-#if defined(LGX_MASK_ABL) && LGX_MASK_ABL == 2
-        return keep;
-#endif
         if (park) {  // park them while slots last
             int c = *scnt();
             for (int j = 0; j < kPend; ++j) {
                 if (((need >> j) & 1u) && c < kSuspSlots) {
-#if !defined(LGX_MASK_ABL) || LGX_MASK_ABL != 3
                     susp_slots(a)[c] = pend_key(pend[j]);
-#endif
                     ++c;
                     keep &= ~(1u << j);
                     need &= ~(1u << j);
@@ -563,7 +485,6 @@ struct WaveTopKT {
             *scnt() = c;
             if (__ballot(need != 0u) == 0ull) return keep;
         }
-        LGX_STAT(9, 1);
         const int64_t m0 = need ? a.mask_indptr[b] : 0, m1 = need ? a.mask_indptr[b + 1] : 0;
         const int32_t* mi = a.mask_indices + m0;
         // the searches run kSearch keys at a time: all kPend at once would hold 5 x kPend registers
@@ -631,13 +552,6 @@ struct WaveTopKT {
     // list updates half by half
     __device__ __forceinline__ void drain(const ScoreArgs& a) {
         if (__ballot(pcnt > 0) == 0ull) return;
-#ifdef LGX_SCORE_STATS
-        const uint64_t dr_t0_ = __builtin_amdgcn_s_memtime();
-        struct DrainStamp {
-            uint64_t* acc; uint64_t t0;
-            __device__ ~DrainStamp() { *acc += __builtin_amdgcn_s_memtime() - t0; }
-        } dr_stamp_{&stat_[21], dr_t0_};
-#endif
         const uint32_t keep = drop_masked(a);
         for (int ph = 0; ph < 2; ++ph) {
             if (__ballot(ph == h && pcnt > 0) == 0ull) continue;
@@ -659,7 +573,6 @@ struct WaveTopKT {
             if (ph == h) {
                 uint32_t todo = cmask;
                 while (todo) {  // one copy of the insertion code, one iteration per survivor
-                    LGX_STAT(18, 1);
                     const int r = __builtin_ctz(todo);
                     todo &= todo - 1;
                     insert_key<true>(a, make_key(pick<NACC>(acc0, acc1, r), item_of<L16>(ib, r)));
@@ -678,9 +591,6 @@ struct WaveTopKT {
     // exact mask test of the parked keys, then the survivors go in half by half
     __device__ __forceinline__ void resolve_suspects(const ScoreArgs& a) {
         if (!park) return;
-#if defined(LGX_MASK_ABL) && LGX_MASK_ABL == 3
-        return;
-#endif
         const int n = user_ok ? *scnt() : 0;
         if (__ballot(n > 0) == 0ull) return;
         const uint64_t* susp = susp_slots(a);
@@ -775,18 +685,19 @@ __global__ __launch_bounds__(WPB * 64) void score_topk_kernel(ScoreArgs a) {
 // Workgroup shape: WAVES x 32 users, tiles of 32*NACC items.  <8, 2> (one 512-thread workgroup per
 // CU, 64-item tiles) is the one launched; see lds_waves() for the measured alternative.
 
-// ABLATE value of the LDS walk that keeps only the global min / max of the scores (no top-k state
-// touched): lgx_score_minmax, the reference's np.max / np.min over the full U x I matrix
-// (recommend.py:163-164, :377).  A product mode, not a development ablation.
-constexpr int kMinMaxOnly = 10;
-// ABLATE value of the walk that writes each user's score floor (ScoreArgs::floor) over the first
+// Modes of the LDS walk.  kTopK: the running top-k (lgx_score_topk).  kMinMaxOnly: only the
+// global min / max of the scores (no top-k state touched): lgx_score_minmax, the reference's np.max /
+// np.min over the full U x I matrix (recommend.py:163-164, :377).
+constexpr int kTopK = 0;
+constexpr int kMinMaxOnly = 1;
+// kFloorOnly: the walk that writes each user's score floor (ScoreArgs::floor) over the first
 // floor_items items of its split instead of a top-k: the items are cut into 64 groups by their
 // position in the 64-item tile, a group holding a masked item of the user is dropped, and the floor
 // is the k-th largest of the remaining group maxima.  Those are k distinct unmasked items scoring
 // at least the floor, so the user's k-th best (over the split, hence over the catalog) is never below
 // it, and a sweep that starts its lists with this threshold drops no item of the exact top-k (ties
 // at the floor included: a filling list takes scores >= floor).  A product mode.
-constexpr int kFloorOnly = 13;
+constexpr int kFloorOnly = 2;
 
 template <int KSTEPS, int WAVES = 8, int NACC = 2, int ESZ = 2>
 struct LdsGeom {
@@ -846,15 +757,12 @@ __device__ __forceinline__ uint32_t lds_u32(const void* p) {
 // mask loads) overlaps its partner's MFMAs.  The late epilogue only reads the accumulators, which
 // stay in registers across the barrier; results are bit for bit those of the unstaggered order.
 //
-// MFMA shape (M16): v_mfma_f32_16x16x32_bf16 holds a higher clock than 32x32x16 on random operands
+// MFMA shape: v_mfma_f32_16x16x32_bf16 holds a higher clock than 32x32x16 on random operands
 // (tools/mfma_peak: 1962 vs 1615 TF/s bare, same FLOPs per cycle).  A wave's 32 users are two
 // 16-user B blocks and its 64-item tile four 16-item A blocks: 8 accumulators of 4 scores.  One
 // v_permlane16_swap per accumulator register then regroups them so that lane l holds 32 scores of
 // user l & 31 (items 16 q + 8 h + 0..7 of block q), the layout the top-k state expects: lanes l and
 // l + 32 still share a user.
-#ifndef LGX_DIRECT_EVENTS  // development A/B: -DLGX_DIRECT_EVENTS=0 keeps the regroup-always event path
-#define LGX_DIRECT_EVENTS 1
-#endif
 //
 // fp32 (DT = LGX_DTYPE_F32, score_topk_f32_lds): the same walk on v_mfma_f32_16x16x4_f32 (exact f32
 // products and sums, the reference's precision).  A 16-B chunk of a row now holds 4 features, and
@@ -864,26 +772,21 @@ __device__ __forceinline__ uint32_t lds_u32(const void* p) {
 // bf16 MFMA rate a 64-item tile is 16 K MFMA cycles per wave, so the workgroup is 4 waves x 32 users,
 // ONE wave per SIMD with the full 512-register file (the 32 users' f32 rows take 128 VGPRs), no
 // stagger (no partner wave to overlap), a 2-buffer ring of 64 KB tiles at d = 256.
-template <int DT, int KSTEPS, bool MINMAX, int ABLATE, int WAVES, int NACC, bool STAGGER, bool M16, int DMAPOS,
-          bool FASTSKIP>
+constexpr int kBf16LdsWaves = 8;
+constexpr int kF32LdsWaves = 4;
+template <int DT, int KSTEPS, bool MINMAX, int MODE, int WAVES, int NACC, bool STAGGER>
 __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreArgs a, int xcd_affine,
                                                     int64_t n_utiles, int nbuf) {
     constexpr bool F32 = DT == LGX_DTYPE_F32;
-    static_assert(!M16 || (NACC == 2 && (F32 || KSTEPS % 2 == 0)), "16x16 path: 64-item tiles, bf16 d a multiple of 32");
-    static_assert(!F32 || M16, "fp32: the 16x16x4 walk only");
+    static_assert(NACC == 2 && (F32 || KSTEPS % 2 == 0), "16x16 walk: 64-item tiles, bf16 d a multiple of 32");
     // SKIP: the fast-path test runs on the MFMA output layout itself (lane l holds 16 scores of user
     // l & 15 and 16 of user 16 + (l & 15)); the regroup into the top-k layout (16 v_permlane16_swap)
     // is paid only by tiles that have a survivor.  Min / max needs every score: not with MINMAX.
-    // development ablations 11 / 12 (tools/score_lab LAB_ABL): 11 = an event is detected and then
-    // dropped (fast path + detection only), 12 = events take the deferred-slot path and the slots are
-    // discarded instead of drained (no drains, no exact path) -- timing only, the lists are wrong
-    constexpr bool LIKE_PRODUCT = ABLATE == 0 || ABLATE == 9 || ABLATE == 11 || ABLATE == 12;
-    constexpr bool SKIP = FASTSKIP && M16 && !MINMAX && LIKE_PRODUCT;
-    constexpr bool DIRECT_EVENTS = LGX_DIRECT_EVENTS != 0;
+    constexpr bool SKIP = !MINMAX && MODE == kTopK;
     typedef LdsGeom<KSTEPS, WAVES, NACC, F32 ? 4 : 2> G;
     typedef Frag<DT> F;
     constexpr int NS = G::CPR / 4;                  // 16x16 walk: chunk groups (k-steps of 4 chunks) per row
-    constexpr int UFN = M16 ? 2 * NS : KSTEPS;      // user fragment registers (16 B each)
+    constexpr int UFN = 2 * NS;                     // user fragment registers (16 B each)
     unsigned char* tiles = smem;  // [nbuf][TILE]
     const int k = a.k;
     const int lane = threadIdx.x & 63;
@@ -911,27 +814,22 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     const bool user_ok = b < a.B;
     uint4 uf[UFN];
     const int r16 = lane & 15, q4 = lane >> 4;
-    if (M16) {  // B fragment (ub, s) at uf[ub * NS + s]: user 16 ub + r16, 16-B chunk 4 s + q4 of its row
+    // B fragment (ub, s) at uf[ub * NS + s]: user 16 ub + r16, 16-B chunk 4 s + q4 of its row
 #pragma unroll
-        for (int ub = 0; ub < 2; ++ub) {
-            const int64_t bu = utile * G::USERS + wave * kUsersPerWave + 16 * ub + r16;
-            const bool ok = bu < a.B;
-            const int64_t qr = ok ? (a.user_rows ? a.user_rows[bu] : bu) : 0;
+    for (int ub = 0; ub < 2; ++ub) {
+        const int64_t bu = utile * G::USERS + wave * kUsersPerWave + 16 * ub + r16;
+        const bool ok = bu < a.B;
+        const int64_t qr = ok ? (a.user_rows ? a.user_rows[bu] : bu) : 0;
 #pragma unroll
-            for (int s2 = 0; s2 < NS; ++s2)
-                uf[ub * NS + s2] = __builtin_bit_cast(uint4, F::load(a.Q, qr, a.d, 2 * s2 + (q4 >> 1), q4 & 1, ok));
-        }
-    } else {
-        const int64_t qrow = user_ok ? (a.user_rows ? a.user_rows[b] : b) : 0;
-#pragma unroll
-        for (int c = 0; c < KSTEPS; ++c) uf[c] = __builtin_bit_cast(uint4, F::load(a.Q, qrow, a.d, c, h, user_ok));
+        for (int s2 = 0; s2 < NS; ++s2)
+            uf[ub * NS + s2] = __builtin_bit_cast(uint4, F::load(a.Q, qr, a.d, 2 * s2 + (q4 >> 1), q4 & 1, ok));
     }
     TopK st;
     st.init(lk, lk + list_keys_per_wave(k), k, lane, b, user_ok);
     st.enable_suspects(a);
     st.build_bloom(a);
     if (a.seed_score) st.seed(a);
-    else if (ABLATE != kFloorOnly && a.floor && user_ok) st.tau = a.floor[b * a.n_splits + split];
+    else if (MODE != kFloorOnly && a.floor && user_ok) st.tau = a.floor[b * a.n_splits + split];
     // consume the prologue loads here: otherwise the compiler treats them as possibly pending at
     // the loop header and waits vmcnt(0) -- i.e. for the tile prefetch -- in every iteration
 #pragma unroll
@@ -944,7 +842,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     for (int w = 0; w < kBloomWords; ++w) asm volatile("" : "+v"(st.bl[w]));
 
     const int64_t i_begin = a.seed_items + (int64_t)split * a.split_items;
-    const int64_t i_end = min(a.n_items, i_begin + (ABLATE == kFloorOnly ? min(a.split_items, a.floor_items) : a.split_items));
+    const int64_t i_end = min(a.n_items, i_begin + (MODE == kFloorOnly ? min(a.split_items, a.floor_items) : a.split_items));
     const int64_t ntiles = i_end > i_begin ? (i_end - i_begin + G::TILE_ITEMS - 1) / G::TILE_ITEMS : 0;
     // single split: every workgroup sweeps the whole catalog, starting at a rotation shared by the
     // workgroups of its XCD (blockIdx mod 8) so that co-resident workgroups read the same tiles
@@ -954,12 +852,8 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     // this wave's pieces of a tile: LDS slot q = piece*64 + lane holds 16-B chunk (q % CPR) of tile
     // row q / CPR, fetched from source chunk (q % CPR) ^ (row & SWZ) (the swizzle lives on the source
     // side because the DMA's LDS destination is lane-linear)
-    // DMAPOS 2 / 3 (development): only the upper / lower half of the waves issues the tile DMA
-    constexpr int DW = DMAPOS == 2 || DMAPOS == 3 ? WAVES / 2 : WAVES;  // 4: all waves, this path
-    constexpr int PPW = (G::PIECES + DW - 1) / DW;
-    const bool issuer = DMAPOS == 2 ? wave >= WAVES / 2 : (DMAPOS == 3 ? wave < WAVES / 2 : true);
-    const int dw = DMAPOS == 2 ? wave - WAVES / 2 : wave;
-    const int my_pieces = issuer ? max(0, min(PPW, G::PIECES - dw * PPW)) : 0;
+    constexpr int PPW = G::PPW;
+    const int my_pieces = max(0, min(PPW, G::PIECES - wave * PPW));
     const uint32_t lds_tiles = lds_u32(tiles);
 
     auto tile_start = [&](int64_t t) {
@@ -977,12 +871,12 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
             const bool tail = t0 + G::TILE_ITEMS > i_end;
             const int last = (int)(i_end - 1 - t0);  // tail rows re-read the split's last row (masked later)
             // offsets recomputed per tile: cheaper than holding them in registers
-            const int q = (dw * PPW + p) * 64 + lane;
+            const int q = (wave * PPW + p) * 64 + lane;
             const int row = q / G::CPR;
             const int src = (q % G::CPR) ^ (row & G::SWZ);
             const int srow = tail && row > last ? last : row;
             lds_dma16(base, (uint32_t)(srow * G::RB + src * 16),
-                      __builtin_amdgcn_readfirstlane(lds_tiles + buf * G::TILE + (dw * PPW + p) * 1024));
+                      __builtin_amdgcn_readfirstlane(lds_tiles + buf * G::TILE + (wave * PPW + p) * 1024));
         }
     };
     auto stage = [&](int buf, int64_t t0) {
@@ -995,7 +889,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(ahead, ntiles) - 1));
     __syncthreads();
     int buf = 0, sbuf = ahead;  // buffer of tile t / of tile t + ahead
-    const bool late = STAGGER && (LIKE_PRODUCT || ABLATE == kFloorOnly) && wave >= WAVES / 2;  // wave-uniform
+    const bool late = STAGGER && MODE != kMinMaxOnly && wave >= WAVES / 2;  // wave-uniform
     f32x16 acc0, acc1;  // late waves: tile t-1's scores, held across the barrier
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     f32x4 c[2][4];      // 16x16x32 accumulators: c[ub][ib] = items 16 ib + 4 (lane >> 4) + reg, user 16 ub + (lane & 15)
@@ -1007,7 +901,6 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         tauB = __shfl(st.tau, 16 + (lane & 15));
     };
     if (SKIP) refresh_taus();
-    if (ABLATE == 9) tauA = tauB = __builtin_huge_valf();  // 9 (development): the fast path alone, no events
     // regroup: swap(X = user block 0, Y = user block 1) between rows 2m and 2m+1 (lanes l, l^16)
     // leaves X' = items 16 ib + 8 h + reg, Y' = items 16 ib + 8 h + 4 + reg of user l & 31
     auto regroup = [&]() {
@@ -1029,95 +922,55 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         }
     };
     // scores of the tile in ring buffer `buf` into acc0 / acc1 (the same code for both wave kinds)
-    // DMAPOS 1: the refill pieces of tile t + ahead are issued between the k-steps of tile t's MFMAs
-    // (piece p after k-step p) instead of all at once before them
-    bool refill = false;
-    int64_t refill_t0 = 0;
     auto compute = [&]() {
         const unsigned char* T = tiles + buf * G::TILE;
-        if constexpr (M16) {
-            constexpr int KS2 = NS;
+        constexpr int KS2 = NS;
 #pragma unroll
-            for (int ub = 0; ub < 2; ++ub)
+        for (int ub = 0; ub < 2; ++ub)
 #pragma unroll
-                for (int ib = 0; ib < 4; ++ib) c[ub][ib] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-            // A fragment (s, ib): item 16 ib + r16, source chunk 4 s + q4 (LDS chunk ^ row swizzle)
-            const unsigned char* rowp = T + r16 * G::RB;
-            auto frag = [&](int s2, int ib) {
-                return *reinterpret_cast<const uint4*>(rowp + ib * 16 * G::RB + (((4 * s2 + q4) ^ (r16 & G::SWZ)) * 16));
-            };
-            // one fragment register per item block: its next k-step is read right after the two
-            // MFMAs that consume it, so every read has the following 6 MFMAs to land
-            uint4 fa[4];
+            for (int ib = 0; ib < 4; ++ib) c[ub][ib] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        // A fragment (s, ib): item 16 ib + r16, source chunk 4 s + q4 (LDS chunk ^ row swizzle)
+        const unsigned char* rowp = T + r16 * G::RB;
+        auto frag = [&](int s2, int ib) {
+            return *reinterpret_cast<const uint4*>(rowp + ib * 16 * G::RB + (((4 * s2 + q4) ^ (r16 & G::SWZ)) * 16));
+        };
+        // one fragment register per item block: its next k-step is read right after the two
+        // MFMAs that consume it, so every read has the following 6 MFMAs to land
+        uint4 fa[4];
 #pragma unroll
-            for (int ib = 0; ib < 4; ++ib) fa[ib] = frag(0, ib);
+        for (int ib = 0; ib < 4; ++ib) fa[ib] = frag(0, ib);
 #pragma unroll
-            for (int s2 = 0; s2 < KS2; ++s2) {
+        for (int s2 = 0; s2 < KS2; ++s2) {
 #pragma unroll
-                for (int ib = 0; ib < 4; ++ib) {
+            for (int ib = 0; ib < 4; ++ib) {
 #pragma unroll
-                    for (int ub = 0; ub < 2; ++ub) {
-                        if constexpr (F32) {
-                            const float4 av = __builtin_bit_cast(float4, fa[ib]);
-                            const float4 bv = __builtin_bit_cast(float4, uf[ub * KS2 + s2]);
-                            c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, c[ub][ib], 0, 0, 0);
-                            c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, c[ub][ib], 0, 0, 0);
-                            c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, c[ub][ib], 0, 0, 0);
-                            c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, c[ub][ib], 0, 0, 0);
-                        } else {
-                            c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                                __builtin_bit_cast(bf16x8, fa[ib]), __builtin_bit_cast(bf16x8, uf[ub * KS2 + s2]),
-                                c[ub][ib], 0, 0, 0);
-                        }
+                for (int ub = 0; ub < 2; ++ub) {
+                    if constexpr (F32) {
+                        const float4 av = __builtin_bit_cast(float4, fa[ib]);
+                        const float4 bv = __builtin_bit_cast(float4, uf[ub * KS2 + s2]);
+                        c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, c[ub][ib], 0, 0, 0);
+                        c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, c[ub][ib], 0, 0, 0);
+                        c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, c[ub][ib], 0, 0, 0);
+                        c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, c[ub][ib], 0, 0, 0);
+                    } else {
+                        c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            __builtin_bit_cast(bf16x8, fa[ib]), __builtin_bit_cast(bf16x8, uf[ub * KS2 + s2]),
+                            c[ub][ib], 0, 0, 0);
                     }
-                    if (s2 + 1 < KS2 && ABLATE != 8) fa[ib] = frag(s2 + 1, ib);  // 8 (development): one read per tile
                 }
-                if (DMAPOS == 1 && s2 < G::PPW && refill) stage_piece(sbuf, refill_t0, s2);
+                if (s2 + 1 < KS2) fa[ib] = frag(s2 + 1, ib);
             }
-            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
-            for (int s2 = 0; s2 < KS2; ++s2) {
+        for (int s2 = 0; s2 < KS2; ++s2) {
 #pragma unroll
-                for (int ib = 0; ib < 4; ++ib) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, F32 ? 8 : 2, 0);
-                    if (s2 + 1 < KS2) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                }
+            for (int ib = 0; ib < 4; ++ib) {
+                __builtin_amdgcn_sched_group_barrier(0x008, F32 ? 8 : 2, 0);
+                if (s2 + 1 < KS2) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
             }
-            if (!SKIP && ABLATE != kMinMaxOnly && ABLATE != kFloorOnly) regroup();
-        } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            acc0[r] = 0.0f;
-            acc1[r] = 0.0f;
         }
-        const int it0 = col, it1 = 32 + col;
-        const unsigned char* r0 = T + it0 * G::RB;
-        const unsigned char* r1 = T + it1 * G::RB;
-        // fragment reads run one k-step ahead of the MFMAs
-        uint4 a0 = *reinterpret_cast<const uint4*>(r0 + ((h ^ (it0 & G::SWZ)) * 16));
-        uint4 a1 = a0;
-        if (NACC == 2) a1 = *reinterpret_cast<const uint4*>(r1 + ((h ^ (it1 & G::SWZ)) * 16));
-#pragma unroll
-        for (int c = 0; c < KSTEPS; ++c) {
-            uint4 n0 = a0, n1 = a1;
-            if (c + 1 < KSTEPS) {
-                const int pch = 2 * (c + 1) + h;
-                n0 = *reinterpret_cast<const uint4*>(r0 + ((pch ^ (it0 & G::SWZ)) * 16));
-                if (NACC == 2) n1 = *reinterpret_cast<const uint4*>(r1 + ((pch ^ (it1 & G::SWZ)) * 16));
-            }
-            acc0 = F::mma(a0, uf[c], acc0);
-            if (NACC == 2) acc1 = F::mma(a1, uf[c], acc1);
-            a0 = n0;
-            a1 = n1;
-        }
-        // keep the reads one k-step ahead: NACC DS reads, then the NACC MFMAs of the previous k-step
-        __builtin_amdgcn_sched_group_barrier(0x100, NACC, 0);
-#pragma unroll
-        for (int c = 0; c < KSTEPS; ++c) {
-            if (c + 1 < KSTEPS) __builtin_amdgcn_sched_group_barrier(0x100, NACC, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, NACC, 0);
-        }
-        }
+        if (!SKIP && MODE == kTopK) regroup();
     };
     // the split's last tile is the only one that can run past i_end: a block variant of its own
     // min / max mode: every score of the tile straight from the MFMA layout.  Rows past the split's
@@ -1167,11 +1020,11 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
             }
     };
     auto epilogue = [&](int64_t e0) {
-        if constexpr (ABLATE == kMinMaxOnly) {
+        if constexpr (MODE == kMinMaxOnly) {
             minmax_tile();
             return;
         }
-        if constexpr (ABLATE == kFloorOnly) {
+        if constexpr (MODE == kFloorOnly) {
             floor_tile(e0);
             return;
         }
@@ -1187,7 +1040,6 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
                         m1 = fmaxf(m1, c[1][ib][r]);
                     }
                 if (__ballot((m0 >= tauA) | (m1 >= tauB)) == 0ull) return;  // wave-uniform fast path
-                if constexpr (ABLATE == 11) return;
                 // maxima of one item block's 4-score groups (both user blocks), re-derived on events
                 auto flagged = [&](int ib) {
                     const float a0 = fmaxf(fmaxf(c[0][ib][0], c[0][ib][1]), fmaxf(c[0][ib][2], c[0][ib][3]));
@@ -1201,7 +1053,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
                 // scores and re-deriving the group maxima.  A lane whose slots would run over goes
                 // down the full path below, which re-appends from pcnt (the writes here only went
                 // to slots at or past it).
-                if (DIRECT_EVENTS && __ballot(st.unbounded()) == 0ull) {
+                if (__ballot(st.unbounded()) == 0ull) {
                     int n = st.pcnt;
                     const uint32_t ibase = (uint32_t)(e0 + 8 * h);
 #pragma unroll
@@ -1222,80 +1074,32 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
                         st.pcnt = n;
                         return;
                     }
-                    if constexpr (ABLATE == 12) {
-                        st.pcnt = 0;
-                        return;
-                    }
                 }
             }
             regroup();
         }
         const float tau_before = st.tau;
-        if (tail) st.template block<MINMAX, NACC, false, M16, true>(a, acc0, acc1, e0, i_end);
-        else st.template block<MINMAX, NACC, false, M16, false>(a, acc0, acc1, e0, i_end);
+        if (tail) st.template block<MINMAX, NACC, true, true>(a, acc0, acc1, e0, i_end);
+        else st.template block<MINMAX, NACC, true, false>(a, acc0, acc1, e0, i_end);
         // the thresholds move only when a drain or a direct insert ran: most events only defer
         // candidates, and skip the two cross-lane reads
-#ifdef LGX_TAU_EAGER  // development A/B (tools/score_lab_eager)
-        if (SKIP) refresh_taus();
-        (void)tau_before;
-#else
         if (SKIP && __ballot(st.tau != tau_before) != 0ull) refresh_taus();
-#endif
     };
     for (int64_t t = 0; t < ntiles; ++t) {
-        LGX_STAT_T0
         const int64_t t0 = tile_start(t);
-        refill = ABLATE != 5 && ABLATE != 7 && ABLATE != 8 && t + ahead < ntiles;
-        if (refill) refill_t0 = tile_start(ABLATE == 6 ? 0 : t + ahead);  // 6 (development): L2-hot refills
-        if (DMAPOS != 1 && refill) stage(sbuf, refill_t0);
-#ifdef LGX_SCORE_STATS
-        const uint64_t ep_t0_ = __builtin_amdgcn_s_memtime();
-#endif
+        if (t + ahead < ntiles) stage(sbuf, tile_start(t + ahead));
         if (late && t > 0) epilogue(prev_t0);
-#ifdef LGX_SCORE_STATS
-        st.stat_[t < 1024 ? 3 : 11] += __builtin_amdgcn_s_memtime() - ep_t0_;
-#endif
         compute();
-#ifdef LGX_SCORE_STATS
-        const uint64_t stat_t1_ = __builtin_amdgcn_s_memtime();
-#endif
-        if (ABLATE == 1 || ABLATE == 5 || ABLATE == 6 || ABLATE == 7 || ABLATE == 8) {  // development: MFMA + LDS pipeline only (5: no refills either) (keeps the accumulators live)
-            float z = 0.0f;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) z += acc0[r] + (NACC == 2 ? acc1[r] : 0.0f);
-            st.mx = fmaxf(st.mx, z);
-        } else if (ABLATE == 3) {  // development: filter fast path only
-            st.template block<MINMAX, NACC, true, M16>(a, acc0, acc1, t0, i_end);
-        } else if (!late) {
-#ifdef LGX_SCORE_STATS
-            const uint64_t ep_t1_ = __builtin_amdgcn_s_memtime();
-#endif
-            epilogue(t0);
-#ifdef LGX_SCORE_STATS
-            st.stat_[t < 1024 ? 3 : 11] += __builtin_amdgcn_s_memtime() - ep_t1_;
-#endif
-        }
+        if (!late) epilogue(t0);
         prev_t0 = t0;
-#ifdef LGX_SCORE_STATS
-        const uint64_t stat_t2_ = __builtin_amdgcn_s_memtime();
-        st.stat_[4] += stat_t2_ - stat_t1_;  // top-k work
-        st.stat_[5] += stat_t1_ - stat_t0_;  // staging + MFMA
-        st.stat_[0] += 1;
-#endif
         // tiles t+2 .. t+ahead may stay in flight; tile t+1 must have landed
-        if (ABLATE != 7 && ABLATE != 8) {  // 7 (development): no refills and no barrier -- the MFMA + LDS-read ceiling
-            wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(t + ahead, ntiles - 1) - (t + 1)));
-            __syncthreads();
-        }
-#ifdef LGX_SCORE_STATS
-        st.stat_[t < 1024 ? 12 : 6] += __builtin_amdgcn_s_memtime() - stat_t2_;  // wait + barrier
-        st.stat_[t < 1024 ? 13 : 14] += 1;
-#endif
+        wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(t + ahead, ntiles - 1) - (t + 1)));
+        __syncthreads();
         buf = buf + 1 == nbuf ? 0 : buf + 1;
         sbuf = sbuf + 1 == nbuf ? 0 : sbuf + 1;
     }
     if (late && ntiles > 0) epilogue(prev_t0);
-    if constexpr (ABLATE == kMinMaxOnly) {
+    if constexpr (MODE == kMinMaxOnly) {
 #pragma unroll
         for (int m = 32; m > 0; m >>= 1) {
             st.mn = fminf(st.mn, __shfl_xor(st.mn, m, 64));
@@ -1307,7 +1111,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         }
         return;
     }
-    if constexpr (ABLATE == kFloorOnly) {
+    if constexpr (MODE == kFloorOnly) {
 #pragma unroll
         for (int ub = 0; ub < 2; ++ub) {
             const int64_t bu = utile * G::USERS + wave * kUsersPerWave + 16 * ub + r16;
@@ -1358,26 +1162,21 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         return;
     }
     st.flush(a, split, lane);
-#ifdef LGX_SCORE_STATS
-    { uint64_t* stat_ = st.stat_; LGX_STAT_FLUSH }
-#endif
 }
 
-template <int KSTEPS, bool MINMAX, int ABLATE = 0, int WAVES = 8, int NACC = 2, bool STAGGER = true, bool M16 = true,
-          int DMAPOS = 0, bool FASTSKIP = true>
-__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
+template <int KSTEPS, bool MINMAX, int MODE = kTopK>
+__global__ __launch_bounds__(kBf16LdsWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    score_topk_lds_body<LGX_DTYPE_BF16, KSTEPS, MINMAX, ABLATE, WAVES, NACC, STAGGER, M16, DMAPOS, FASTSKIP>(
+    score_topk_lds_body<LGX_DTYPE_BF16, KSTEPS, MINMAX, MODE, kBf16LdsWaves, 2, true>(
         smem, a, xcd_affine, n_utiles, nbuf);
 }
 
-constexpr int kF32LdsWaves = 4;
 template <int KSTEPS, bool MINMAX, int MODE = 0>
 __global__ __launch_bounds__(kF32LdsWaves * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void score_topk_f32_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    score_topk_lds_body<LGX_DTYPE_F32, KSTEPS, MINMAX, MODE, kF32LdsWaves, 2, false, true, 0, true>(
+    score_topk_lds_body<LGX_DTYPE_F32, KSTEPS, MINMAX, MODE, kF32LdsWaves, 2, false>(
         smem, a, xcd_affine, n_utiles, nbuf);
 }
 
@@ -1449,12 +1248,14 @@ __global__ void minmax_init(uint32_t* mm) {
 constexpr int kDenseWaves = 8;
 constexpr int kDenseUsers = kDenseWaves * kUsersPerWave;
 
-template <int DT, int KCH>
+// SIG: the reference's sigmoid (model.py:183) as a template parameter: a runtime flag let the
+// compiler evaluate expf for every score and select (profiles/r03_a6_runtime_sigmoid_flag.json,
+// r03_a6_sigmoid_template.json: 3.83 -> 3.61 ms at [4096, 1M] d=256 bf16 on one box)
+template <int DT, int KCH, bool SIG>
 __global__ __launch_bounds__(kDenseWaves * 64) void score_dense_kernel(const void* Q, const int64_t* user_rows,
                                                                         const void* items, int64_t B, int64_t n_items,
-                                                                        int64_t d, int apply_sigmoid,
-                                                                        float* __restrict__ out, int64_t n_ug,
-                                                                        int64_t split_items) {
+                                                                        int64_t d, float* __restrict__ out,
+                                                                        int64_t n_ug, int64_t split_items) {
     typedef Frag<DT> F;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, col = lane & 31;
@@ -1492,7 +1293,7 @@ __global__ __launch_bounds__(kDenseWaves * 64) void score_dense_kernel(const voi
             const int64_t u = u0 + tile_row(r, h);
             if (u < B) {
                 const float sc = acc[r];
-                out[u * n_items + item_row] = apply_sigmoid ? 1.0f / (1.0f + expf(-sc)) : sc;
+                out[u * n_items + item_row] = SIG ? 1.0f / (1.0f + expf(-sc)) : sc;
             }
         }
     }
@@ -1517,11 +1318,11 @@ __host__ __device__ constexpr int dense_waves_per_simd(int dt, int kch) {
     return kch <= (dt == LGX_DTYPE_BF16 ? 16 : 8) ? 4 : 2;
 }
 
-template <int DT, int KCH>
+template <int DT, int KCH, bool SIG>
 __global__ __launch_bounds__(kDenseWaves * 64)
 __attribute__((amdgpu_waves_per_eu(dense_waves_per_simd(DT, KCH), dense_waves_per_simd(DT, KCH))))
 void score_dense_lds(const void* Q, const int64_t* user_rows, const void* items, int64_t B, int64_t n_items,
-                     int64_t d, int apply_sigmoid, float* __restrict__ out, int64_t n_ug, int64_t split_items) {
+                     int64_t d, float* __restrict__ out, int64_t n_ug, int64_t split_items) {
     static_assert(KCH >= 8, "swizzle needs >= 16 slots per row");
     typedef Frag<DT> F;
     constexpr int SPR = 2 * KCH;           // 16-B slots per item row (a chunk = 32 B = two halves)
@@ -1594,7 +1395,7 @@ void score_dense_lds(const void* Q, const int64_t* user_rows, const void* items,
                     if (u0 + tile_row(r, h) < B) {
                         const float sc = acc[r];
                         char* base = reinterpret_cast<char*>(out + (u0 + tile_row(r, 0)) * n_items + i0);
-                        *reinterpret_cast<float*>(base + boff) = apply_sigmoid ? 1.0f / (1.0f + expf(-sc)) : sc;
+                        *reinterpret_cast<float*>(base + boff) = SIG ? 1.0f / (1.0f + expf(-sc)) : sc;
                     }
                 }
             }
@@ -1825,7 +1626,7 @@ struct SplitPlan {
 // doubles the barriers per MFMA, which costs more than the overlap of two independent workgroups
 // recovers.  f32: <4 waves, 64-item tiles>, one workgroup (one wave per SIMD) per CU.  Either way one
 // workgroup per CU, 256 resident.
-inline int lds_waves(int dtype) { return dtype == LGX_DTYPE_F32 ? kF32LdsWaves : 8; }
+inline int lds_waves(int dtype) { return dtype == LGX_DTYPE_F32 ? kF32LdsWaves : kBf16LdsWaves; }
 inline int64_t lds_resident() { return 256; }
 
 constexpr size_t kLdsBytes = 160 * 1024;
@@ -1917,45 +1718,27 @@ int launch_v1(const ScoreArgs& a, int kch, hipStream_t stream) {
 // tile buffers of the LDS kernel: as many as fit beside the top-k lists in the workgroup's share of
 // the CU's LDS, 2..4
 inline int lds_ring_buffers(size_t tile, size_t lists, int wg_per_cu) {
-#ifdef LGX_LAB_NBUF  // development A/B (tools/Makefile score_lab_nb2): a fixed ring depth
-    return LGX_LAB_NBUF;
-#endif
     const size_t budget = kLdsBytes / wg_per_cu;
     const size_t fit = lists < budget ? (budget - lists) / tile : 0;
     return (int)std::max<size_t>(2, std::min<size_t>(4, fit));
 }
 
-template <int KS, bool MM, int ABL, int WAVES, int NACC, bool STAGGER, bool M16, int DMAPOS = 0, bool SKIP = true>
-int launch_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
-    typedef LdsGeom<KS, WAVES, NACC> G;
-    const size_t lists = (size_t)WAVES * list_bytes_per_wave(a.k, kPendBf16Lds);
+template <int KS, bool MM, int MODE>
+int launch_bf16_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
+    typedef LdsGeom<KS, kBf16LdsWaves, 2> G;
+    const size_t lists = (size_t)kBf16LdsWaves * list_bytes_per_wave(a.k, kPendBf16Lds);
     const int nbuf = lds_ring_buffers(G::TILE, lists, 1);
     const size_t shmem = (size_t)nbuf * G::TILE + lists;
-    int rc = set_lds_limit(score_topk_bf16_lds<KS, MM, ABL, WAVES, NACC, STAGGER, M16, DMAPOS, SKIP>, shmem);
+    int rc = set_lds_limit(score_topk_bf16_lds<KS, MM, MODE>, shmem);
     if (rc) return rc;
     const unsigned grid = (unsigned)(p.n_utiles * p.n_splits);
-    score_topk_bf16_lds<KS, MM, ABL, WAVES, NACC, STAGGER, M16, DMAPOS, SKIP><<<grid, WAVES * 64, shmem, stream>>>(
-        a, p.xcd_affine ? 1 : 0, p.n_utiles, nbuf);
+    score_topk_bf16_lds<KS, MM, MODE><<<grid, kBf16LdsWaves * 64, shmem, stream>>>(a, p.xcd_affine ? 1 : 0,
+                                                                                    p.n_utiles, nbuf);
     LGX_LAUNCH_CHECK();
     return LGX_OK;
 }
 
-template <int KS, bool MM, int ABL, int WAVES, int NACC>
-int launch_lds_shape(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
-#ifdef LGX_DEV_SWITCHES
-    // development builds only (tools/Makefile): LGX_SCORE_NOSTAGGER=1 runs the lockstep order,
-    // LGX_SCORE_MFMA32=1 the 32x32x16 main loop; the product library never reads the environment
-    static const char* ns = getenv("LGX_SCORE_NOSTAGGER");
-    static const char* m32 = getenv("LGX_SCORE_MFMA32");
-    if constexpr (ABL == 0 && KS == 16) {  // d = 256 (the C5 shape) only: keeps the build short
-        if (m32 && m32[0] == '1') return launch_lds_kernel<KS, MM, ABL, WAVES, NACC, true, false>(a, p, stream);
-        if (ns && ns[0] == '1') return launch_lds_kernel<KS, MM, ABL, WAVES, NACC, false, true>(a, p, stream);
-    }
-#endif
-    return launch_lds_kernel<KS, MM, ABL, WAVES, NACC, true, true>(a, p, stream);
-}
-
-template <int KS, bool MM, int MODE = 0>
+template <int KS, bool MM, int MODE>
 int launch_f32_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     typedef LdsGeom<KS, kF32LdsWaves, 2, 4> G;
     const size_t lists = (size_t)kF32LdsWaves * list_bytes_per_wave(a.k);
@@ -1974,36 +1757,29 @@ int launch_f32_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t st
     return LGX_OK;
 }
 
-template <bool MM, int ABL = 0>
+template <bool MM, int MODE = kTopK>
 int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream, int dtype = LGX_DTYPE_BF16) {
     const int ksteps = (int)(a.d / 16);
-    if constexpr (ABL == kFloorOnly) {
+    if constexpr (MODE == kFloorOnly) {
         if (dtype == LGX_DTYPE_F32) {
             set_error("lgx_score_topk: score floors are a bf16 LDS kernel mode");
             return LGX_ERR_UNSUPPORTED;
         }
     }
-    if constexpr (ABL == 0 || ABL == kMinMaxOnly) {
+    if constexpr (MODE != kFloorOnly) {
         if (dtype == LGX_DTYPE_F32) {
             switch (ksteps) {
-                case 4: return launch_f32_lds_kernel<4, MM, ABL>(a, p, stream);
-                case 8: return launch_f32_lds_kernel<8, MM, ABL>(a, p, stream);
-                case 12: return launch_f32_lds_kernel<12, MM, ABL>(a, p, stream);
-                case 16: return launch_f32_lds_kernel<16, MM, ABL>(a, p, stream);
+                case 4: return launch_f32_lds_kernel<4, MM, MODE>(a, p, stream);
+                case 8: return launch_f32_lds_kernel<8, MM, MODE>(a, p, stream);
+                case 12: return launch_f32_lds_kernel<12, MM, MODE>(a, p, stream);
+                case 16: return launch_f32_lds_kernel<16, MM, MODE>(a, p, stream);
                 default:
                     set_error("lgx_score_topk: no f32 LDS kernel for d=%lld", (long long)a.d);
                     return LGX_ERR_UNSUPPORTED;
             }
         }
     }
-    if constexpr (ABL != 0 && ABL != kMinMaxOnly && ABL != kFloorOnly) {  // development ablations: d = 256 only
-        if (ksteps != 16) {
-            set_error("lgx_score_topk: ablation builds exist for d=256 only");
-            return LGX_ERR_UNSUPPORTED;
-        }
-        return launch_lds_shape<16, MM, ABL, 8, 2>(a, p, stream);
-    }
-#define LGX_SL(KS) return launch_lds_shape<KS, MM, ABL, 8, 2>(a, p, stream)
+#define LGX_SL(KS) return launch_bf16_lds_kernel<KS, MM, MODE>(a, p, stream)
     switch (ksteps) {
         case 2: LGX_SL(2);
         case 4: LGX_SL(4);
@@ -2160,16 +1936,6 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
         LGX_LAUNCH_CHECK();
     }
     const bool mm = minmax_out != nullptr;
-#ifdef LGX_DEV_SWITCHES
-    // development builds only (tools/Makefile): LGX_SCORE_ABLATE=1 drops the top-k work, =3 keeps
-    // only its fast-path filter, =4 hides the mask from the scoring kernel, =5: =1 without the tile
-    // refills.  The product library has none of these (no getenv, no ablation instantiations).
-    static const char* abl_env = getenv("LGX_SCORE_ABLATE");
-    static const bool ablate = abl_env && abl_env[0] == '1';
-    static const bool ablate3 = abl_env && abl_env[0] == '3';
-    static const bool ablate4 = abl_env && abl_env[0] == '4';
-    static const bool ablate5 = abl_env && abl_env[0] == '5';
-#endif
     const size_t esz = dtype == LGX_DTYPE_F32 ? 4 : 2;
     for (int i = 0; i < n_ranges; ++i) {
         const UserRange& R = ranges[i];
@@ -2189,15 +1955,6 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
             rc = launch_lds<false, kFloorOnly>(a, p, stream, dtype);
             if (rc) return rc;
         }
-#ifdef LGX_DEV_SWITCHES
-        ScoreArgs ka = a;
-        if (ablate4) ka.mask_indptr = nullptr;
-        if (p.lds && ablate4) rc = launch_lds<false>(ka, p, stream);
-        else if (p.lds && ablate) rc = launch_lds<false, 1>(a, p, stream);
-        else if (p.lds && ablate3) rc = launch_lds<false, 3>(a, p, stream);
-        else if (p.lds && ablate5) rc = launch_lds<false, 5>(a, p, stream);
-        else
-#endif
         if (seeded_sweep(p, mm, n_items)) {
             rc = LGX_OK;
             for (int64_t lo = 0, hi = kSeedItems; lo < n_items && rc == LGX_OK; lo = hi, hi *= 2) {
@@ -2300,15 +2057,23 @@ extern "C" int lgx_score_dense(const void* Q, const int64_t* user_rows, const vo
     LGX_REQUIRE(grid < (1LL << 31), LGX_ERR_UNSUPPORTED, "lgx_score_dense: %lld users is too many", (long long)B);
     LGX_REQUIRE(n_items < (1LL << 27), LGX_ERR_UNSUPPORTED, "lgx_score_dense: %lld items is too many (< 2^27)",
                 (long long)n_items);
-#define LGX_SD(DTV, KC)                                                                                    \
-    if constexpr (KC >= 8)                                                                                 \
-        score_dense_lds<DTV, KC><<<(unsigned)grid, kDenseWaves * 64, 0, stream>>>(Q, user_rows, items, B,   \
-                                                                                  n_items, d, apply_sigmoid, \
-                                                                                  scores, n_ug, split_items); \
-    else                                                                                                   \
-        score_dense_kernel<DTV, KC><<<(unsigned)grid, kDenseWaves * 64, 0, stream>>>(Q, user_rows, items, B, \
-                                                                                     n_items, d, apply_sigmoid, \
-                                                                                     scores, n_ug, split_items)
+#define LGX_SD3(DTV, KC, SG)                                                                                   \
+    if constexpr (KC >= 8)                                                                                     \
+        score_dense_lds<DTV, KC, SG><<<(unsigned)grid, kDenseWaves * 64, 0, stream>>>(Q, user_rows, items, B,   \
+                                                                                      n_items, d, scores, n_ug,  \
+                                                                                      split_items);              \
+    else                                                                                                       \
+        score_dense_kernel<DTV, KC, SG><<<(unsigned)grid, kDenseWaves * 64, 0, stream>>>(Q, user_rows, items, B, \
+                                                                                         n_items, d, scores, n_ug, \
+                                                                                         split_items)
+#define LGX_SD(DTV, KC)                  \
+    do {                                 \
+        if (apply_sigmoid) {             \
+            LGX_SD3(DTV, KC, true);      \
+        } else {                         \
+            LGX_SD3(DTV, KC, false);     \
+        }                                \
+    } while (0)
 #define LGX_SD_ALL(DTV)                  \
     switch (kch) {                       \
         case 2: LGX_SD(DTV, 2); break;   \
@@ -2320,6 +2085,7 @@ extern "C" int lgx_score_dense(const void* Q, const int64_t* user_rows, const vo
     if (dtype == LGX_DTYPE_F32) { LGX_SD_ALL(LGX_DTYPE_F32) } else { LGX_SD_ALL(LGX_DTYPE_BF16) }
 #undef LGX_SD_ALL
 #undef LGX_SD
+#undef LGX_SD3
     LGX_LAUNCH_CHECK();
     return LGX_OK;
 }

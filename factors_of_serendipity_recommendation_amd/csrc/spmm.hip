@@ -21,8 +21,10 @@
 //     materialised;
 //   * bf16 storage (LGX_DTYPE_BF16) halves the gathered bytes; arithmetic is fp32 throughout;
 //   * optional column blocking of the item rows (lgx_csr cb_*): they gather the large user table,
-//     so they run as a few launches, each over one column range of every item row, whose slice of
-//     the table fits the Infinity Cache; the row sums are carried in an f32 scratch between them.
+//     so they run as a few launches, each over one column range of every item row, so that one
+//     launch's gathers fall in a 1/nb slice of the table (640 MiB at C4 f32: NOT Infinity-Cache
+//     resident -- the MALL is 256 MiB -- but a narrower working set for the L2s and the MALL, which
+//     measured 57.2 -> 53.6 ms per layer); the row sums are carried in an f32 scratch between them.
 #include "lgx_common.h"
 
 namespace lgx {
@@ -30,25 +32,10 @@ namespace {
 
 constexpr int kThreads = 256;
 
-// LGX_SPMM_NT (development builds only, tools/Makefile): stream the CSR arrays with
-// non-temporal loads so that they do not displace gathered table rows from L2 / MALL
-#ifdef LGX_SPMM_NT
-template <typename V>
-__device__ __forceinline__ V stream_load(const V* p) { return __builtin_nontemporal_load(p); }
-#else
+// the CSR arrays are plain loads: non-temporal CSR streams and non-temporal cold-column gathers
+// measured neutral (profiles/r02_spmm_nt_probe.txt)
 template <typename V>
 __device__ __forceinline__ V stream_load(const V* p) { return *p; }
-#endif
-// LGX_SPMM_NT_COLD (development builds only): gathers of columns >= g_nt_cut (the cold tail of a
-// degree-ordered numbering) are non-temporal, so that they do not displace the hot rows
-#ifdef LGX_SPMM_NT_COLD
-__device__ int g_nt_cut[3] = {0x7fffffff, 0x7fffffff, 0x7fffffff};  // cold: [c0, c1) or >= c2
-typedef uint32_t nt_u32x4 __attribute__((ext_vector_type(4)));
-template <typename R>
-__device__ __forceinline__ R nt_load16(const void* p) {
-    return __builtin_bit_cast(R, __builtin_nontemporal_load(reinterpret_cast<const nt_u32x4*>(p)));
-}
-#endif
 
 template <typename T>
 struct Vec;
@@ -267,17 +254,9 @@ __global__ __launch_bounds__(kThreads) void spmm_segments(LayerArgs a) {
                 const int col = __shfl(my_col, src < n ? src : 0, G);
                 w[u] = src < n ? __shfl(my_val, src, G) : 0.0f;
                 const T* xr = X + (int64_t)col * d;
-#ifdef LGX_SPMM_NT_COLD
-                const bool cold = (col >= g_nt_cut[0] && col < g_nt_cut[1]) || col >= g_nt_cut[2];
-#endif
 #pragma unroll
                 for (int c = 0; c < CPL; ++c) {
                     const int64_t off = (int64_t)(c * G + gl) * VEC;
-#ifdef LGX_SPMM_NT_COLD
-                    if (src < n && off < d && cold)
-                        x[u][c] = nt_load16<typename Vec<T>::raw>(xr + off);
-                    else
-#endif
                     if (src < n && off < d) x[u][c] = Vec<T>::load_raw(xr + off);
                     else x[u][c] = typename Vec<T>::raw{};
                 }
@@ -586,6 +565,25 @@ __global__ __launch_bounds__(kThreads) void layer_epilogue_kernel(LayerArgs a, c
     }
     finish_chunk<T>(a, row, off, v);
 }
+// Cross-rank sum of the push partials of the sharded layer (distributed.py): dst = src[0] + src[1]
+// + ... + src[n-1], added left to right in fp32, slab j at src + j * slab_elems.  One fixed order,
+// so the sum does not depend on how the exchange was chunked or which collective moved the slabs
+// (a reduce-scatter's order follows its ring / channel assignment).  HBM-bound: n + 1 slab passes.
+__global__ __launch_bounds__(kThreads) void sum_slabs_kernel(const float* __restrict__ src, int64_t n_slabs,
+                                                             int64_t slab_elems, int64_t n4, float* __restrict__ dst) {
+    const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;  // float4 index
+    if (i >= n4) return;
+    float4 acc = reinterpret_cast<const float4*>(src)[i];
+    for (int64_t j = 1; j < n_slabs; ++j) {
+        const float4 v = reinterpret_cast<const float4*>(src + j * slab_elems)[i];
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+    }
+    reinterpret_cast<float4*>(dst)[i] = acc;
+}
+
 }  // namespace
 }  // namespace lgx
 
@@ -616,6 +614,20 @@ extern "C" int lgx_layer_epilogue(const float* y, int64_t rows, void* Y, const v
     const unsigned grid = (unsigned)ceil_div(chunks, (int64_t)kThreads);
     if (dtype == LGX_DTYPE_F32) layer_epilogue_kernel<float><<<grid, kThreads, 0, as_hip(stream)>>>(a, y, rows);
     else layer_epilogue_kernel<uint16_t><<<grid, kThreads, 0, as_hip(stream)>>>(a, y, rows);
+    LGX_LAUNCH_CHECK();
+    return LGX_OK;
+}
+
+extern "C" int lgx_sum_slabs(const float* src, int64_t n_slabs, int64_t slab_elems, float* dst,
+                             lgx_stream_t stream) {
+    LGX_REQUIRE(n_slabs >= 1 && slab_elems >= 0 && (slab_elems == 0 || (src && dst)), LGX_ERR_INVALID_ARG,
+                "lgx_sum_slabs: bad arguments");
+    LGX_REQUIRE(slab_elems % 4 == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0,
+                LGX_ERR_UNSUPPORTED, "lgx_sum_slabs: slabs must be whole, 16-B aligned float4 runs");
+    if (slab_elems == 0) return LGX_OK;
+    const int64_t n4 = slab_elems / 4;
+    sum_slabs_kernel<<<(unsigned)ceil_div(n4, (int64_t)kThreads), kThreads, 0, as_hip(stream)>>>(src, n_slabs,
+                                                                                              slab_elems, n4, dst);
     LGX_LAUNCH_CHECK();
     return LGX_OK;
 }
@@ -694,11 +706,3 @@ extern "C" int lgx_propagate(const lgx_csr* A, const void* E0, float* out, int64
     }
     return LGX_OK;
 }
-
-#ifdef LGX_SPMM_NT_COLD
-extern "C" int lgx_dev_set_nt_cut(int c0, int c1, int c2) {
-    const int cut[3] = {c0, c1, c2};
-    LGX_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_nt_cut), cut, sizeof(cut)));
-    return LGX_OK;
-}
-#endif

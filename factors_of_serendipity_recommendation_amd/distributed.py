@@ -14,23 +14,35 @@ edges twice:
 Layer k.  With U (10M) >> I (1M) the user table is the big one, so it never moves:
   * users pull:  U^k[own] = A_pull . I^{k-1}  -- needs the full item table (all-gathered, I*d*s bytes)
   * items push:  P = A_push . U^{k-1}[own]    -- fp32 partial sums for EVERY item from this rank's
-                 users only; reduce_scatter(SUM) leaves each rank the total of its own item block;
-                 the layer epilogue (bf16 store, layer sum, mean) runs on that block, which is then
+                 users only; an all-to-all hands rank q the partials of its own item block, which it
+                 adds in rank order (lgx_sum_slabs: a reduce-scatter whose sum does not depend on
+                 the collective's ring / channel order, nor on the chunking below); the layer
+                 epilogue (bf16 store, layer sum, mean) runs on that block, which is then
                  all-gathered for the next pull.
 Per rank and layer the wire carries ~(world-1)/world * I*d*(4 + s) bytes, against
 (world-1)/world * (U + I)*d*s for all-gathering both tables: 3.7x less at C4 (10M x 1M, d=128 bf16).
 
-Overlap.  The reduce-scatter of layer k runs under the pull of layer k; the all-gather of item
-layer k runs under the push of layer k+1.  The last layer is never gathered: each rank keeps the
-fp32 layer means of its own users and items (gather_outputs() assembles the full tables).
+Overlap.  The push runs in n_chunks launches, chunk c covering rows [c*mc, (c+1)*mc) of EVERY
+rank's item block (its rows re-ordered chunk-major, so a chunk's partials are one contiguous
+[world, mc, d] slab set); chunk c's exchange starts while chunks c+1.. compute, and the exchanges
+finish under the pull of layer k; the all-gather of item layer k runs under the push of layer k+1.
+A chunk's rows keep the unchunked operator's segment length, so every row is summed exactly as in
+one launch: chunked and unchunked layers are equal bit for bit.  The last layer is never gathered:
+each rank keeps the fp32 layer means of its own users and items (gather_outputs() assembles the
+full tables).
+
+Diagnostics.  With record_phases set, every step stamps the compute stream after each phase
+(push, allgather_wait, pull, exchange_wait, reduce, epilogue); the waits are the time the stream
+sat behind a collective, i.e. the communication the schedule left exposed (phase_summary()).
 
 The SpMM and epilogue callables are injectable so that the CPU tests drive the same schedule over
 gloo with an oracle SpMM.
 """
 from __future__ import annotations
 
+import time
 from dataclasses import dataclass
-from typing import Callable, List, Optional, Tuple
+from typing import Callable, Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -162,6 +174,76 @@ def pad_table(full: torch.Tensor, bounds: np.ndarray, pad: int) -> torch.Tensor:
     return out
 
 
+def _row_gather(G: CSRGraph, rows: torch.Tensor, seg_len: Optional[int]) -> CSRGraph:
+    """The rows `rows` of G, in that order, as a CSR (columns keep their order within each row)."""
+    dev = G.indptr.device
+    rows = rows.to(device=dev, dtype=torch.int64)
+    lens = torch.diff(G.indptr)[rows]
+    indptr = torch.zeros(rows.numel() + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(lens, 0, out=indptr[1:])
+    rid = torch.repeat_interleave(torch.arange(rows.numel(), device=dev, dtype=torch.int64), lens)
+    pos = G.indptr[rows][rid] + torch.arange(rid.numel(), device=dev, dtype=torch.int64) - indptr[rid]
+    return CSRGraph(indptr, G.indices[pos].contiguous(), G.vals[pos].contiguous(), rows.numel(), G.n_cols)
+
+
+def chunk_push_operator(A_push: CSRGraph, world: int, mi: int, n_chunks: int) -> List[Tuple[CSRGraph, int, int]]:
+    """Cut the push operator (world * mi item rows) into chunks: chunk c = rows q*mi + c*mc + j of
+    every rank block q (j < its mc_c rows), in (q, j) order, so that its output is the [world, mc_c,
+    d] slab set one all-to-all exchanges.  Returns [(operator, first row of the chunk in a block,
+    mc_c)].  Every chunk keeps A_push's segment length, so each row is summed as in one launch."""
+    mc = max(1, -(-mi // max(1, n_chunks)))
+    seg_len = A_push.plan.seg_len if A_push.plan is not None else None
+    out = []
+    dev = A_push.indptr.device
+    for c0 in range(0, mi, mc):
+        m = min(mc, mi - c0)
+        rows = (torch.arange(world, dtype=torch.int64)[:, None] * mi + c0 + torch.arange(m)[None, :]).reshape(-1)
+        G = _row_gather(A_push, rows.to(dev), seg_len)
+        G.plan = make_plan(G.indptr.cpu().numpy(), seg_len)
+        G.ensure_plan()
+        out.append((G, c0, m))
+    return out
+
+
+class PhaseRecorder:
+    """Per-step stamps on the compute stream (HIP events; host clock for CPU tensors): the time
+    between two stamps is charged to the label of the later one."""
+
+    def __init__(self, cuda: bool):
+        self.cuda = cuda
+        self.steps: List[List[Tuple[str, object]]] = []
+        self._cur: Optional[List[Tuple[str, object]]] = None
+
+    def _stamp(self):
+        if self.cuda:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            return ev
+        return time.perf_counter()
+
+    def begin(self) -> None:
+        self._cur = [("begin", self._stamp())]
+
+    def mark(self, label: str) -> None:
+        if self._cur is not None:
+            self._cur.append((label, self._stamp()))
+
+    def end(self) -> None:
+        if self._cur is not None:
+            self.steps.append(self._cur)
+            self._cur = None
+
+    def summary(self) -> Dict[str, float]:
+        """Mean milliseconds per step by label (call after the stream has drained)."""
+        tot: Dict[str, float] = {}
+        for st in self.steps:
+            for (_, a), (label, b) in zip(st[:-1], st[1:]):
+                dt = a.elapsed_time(b) if self.cuda else (b - a) * 1e3
+                tot[label] = tot.get(label, 0.0) + dt
+        n = max(1, len(self.steps))
+        return {k: v / n for k, v in tot.items()}
+
+
 LayerFn = Callable[..., None]
 
 
@@ -180,20 +262,37 @@ def _default_stack_fn(A, X, E0, prev, out, n_mean):
     propagate_layer_stack(A, X, E0, prev, out, n_mean)
 
 
+def _default_sum_fn(src, out):
+    from .ops import sum_slabs
+    sum_slabs(src, out)
+
+
+def _host_sum(src, out):
+    """lgx_sum_slabs' order on the host (CPU tests): src[0] + src[1] + ... left to right."""
+    acc = src[0].clone()
+    for j in range(1, src.shape[0]):
+        acc += src[j]
+    out.copy_(acc)
+
+
 class ShardedPropagation:
     """K-layer LightGCN propagation of a row-sharded graph (see module docstring)."""
 
     def __init__(self, shard: Shard, E0_user: torch.Tensor, E0_item: torch.Tensor, K: int,
                  group=None, layer_fn: Optional[LayerFn] = None, epilogue_fn: Optional[LayerFn] = None,
-                 stack_fn: Optional[LayerFn] = None, force_collectives: bool = False):
+                 stack_fn: Optional[LayerFn] = None, force_collectives: bool = False,
+                 n_chunks: Optional[int] = None, sum_fn: Optional[Callable] = None):
         """E0_user / E0_item: the FULL layer-0 tables in global row order (replicated input, as every
         rank holds the embedding parameters); dtype f32 or bf16.  The user side keeps its K-1 layer
         tables and forms the mean in the last pull (stack_fn = lgx_propagate_layer_stack), as the
         single-GPU lgx_propagate does; the item side keeps the f32 running sum of its own block.
 
-        force_collectives: issue the reduce-scatter / all-gather even at world 1 (where they are
-        copies), so that a one-GPU RCCL group runs the async collective stream ordering the
-        overlap depends on."""
+        force_collectives: issue the exchange / all-gather even at world 1 (where they are copies),
+        so that a one-GPU RCCL group runs the async collective stream ordering the overlap depends on.
+
+        n_chunks: push launches per layer (default 4 with collectives, else 1), each followed by its
+        own all-to-all.  sum_fn(src [n, rows, d], out [rows, d]): the ordered slab sum (default
+        lgx_sum_slabs on the GPU, the same left-to-right adds on the host)."""
         self.s = shard
         self.K = K
         self.group = group
@@ -219,8 +318,17 @@ class ShardedPropagation:
         self.out_u = torch.zeros((s.n_u_local, d), dtype=torch.float32, device=dev)
         self.out_i = torch.zeros((s.n_i_local, d), dtype=torch.float32, device=dev)
         self._collective = s.world > 1 or force_collectives
-        # gloo cannot reduce-scatter device tensors: all-reduce + slice there (tests only)
-        self._rs_native = self._collective and not (dev.type == "cuda" and dist.get_backend(group) == "gloo")
+        # gloo has no all-to-all of device tensors: an all-gather of the slabs there (tests and
+        # rehearsals only), the same slabs in the same order, hence the same sums
+        self._a2a_native = self._collective and not (dev.type == "cuda" and dist.get_backend(group) == "gloo")
+        if n_chunks is None:
+            n_chunks = 4 if self._collective else 1
+        self.push_chunks = chunk_push_operator(s.A_push, s.world, s.mi, n_chunks) if n_chunks > 1 else \
+            [(s.A_push, 0, s.mi)]
+        self.R = torch.zeros_like(self.P)  # received partials: chunk c = [world, mc_c, d] slabs
+        self.sum_fn = sum_fn or (_default_sum_fn if dev.type == "cuda" else _host_sum)
+        self.record_phases = False
+        self.phases = PhaseRecorder(dev.type == "cuda")
 
     @staticmethod
     def _buf(k: int) -> int:
@@ -235,17 +343,31 @@ class ShardedPropagation:
             return _lib.LGX_LAYER_LAST
         return _lib.LGX_LAYER_MID
 
-    def _reduce_scatter(self):
-        """yi = this rank's block of sum over ranks of P."""
+    def _chunk_views(self, c0: int, m: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        """P / R storage of the chunk starting at block row c0: [world, m, d] each, contiguous."""
+        w, d = self.s.world, self.d
+        off = w * c0 * d
+        n = w * m * d
+        return self.P.view(-1)[off:off + n].view(w, m, d), self.R.view(-1)[off:off + n].view(w, m, d)
+
+    def _exchange(self, c0: int, m: int):
+        """Rank q receives slab r of every rank r's chunk (the partials of q's own item rows)."""
+        P, R = self._chunk_views(c0, m)
         if not self._collective:
-            self.yi.copy_(self.P)
+            R.copy_(P)
             return None
-        if self._rs_native:
-            return dist.reduce_scatter_tensor(self.yi, self.P, group=self.group, async_op=True)
-        dist.all_reduce(self.P, group=self.group)
-        r, mi = self.s.rank, self.s.mi
-        self.yi.copy_(self.P[r * mi:(r + 1) * mi])
+        if self._a2a_native:
+            return dist.all_to_all_single(R, P, group=self.group, async_op=True)
+        w, r = self.s.world, self.s.rank
+        allp = torch.empty((w * w * m, self.d), dtype=P.dtype, device=P.device)
+        dist.all_gather_into_tensor(allp, P.reshape(w * m, self.d), group=self.group)
+        R.copy_(allp.view(w, w, m, self.d)[:, r])
         return None
+
+    def _reduce(self, c0: int, m: int) -> None:
+        """yi[c0:c0+m] = sum over ranks of the received slabs, in rank order."""
+        _, R = self._chunk_views(c0, m)
+        self.sum_fn(R, self.yi[c0:c0 + m])
 
     def _all_gather(self, table: torch.Tensor):
         if not self._collective:
@@ -264,15 +386,26 @@ class ShardedPropagation:
         """One full propagation; returns this rank's (out_user, out_item) fp32 layer means."""
         s = self.s
         n_mean = float(self.K + 1)
+        rec = self.phases if self.record_phases else None
+        if rec:
+            rec.begin()
         ag = None  # all-gather publishing the item table of the previous layer
         for k in range(1, self.K + 1):
             mode = self._mode(k)
-            # push: item partial sums from this rank's users at layer k-1
-            self.layer_fn(s.A_push, self.Xu[k - 1], _lib.LGX_LAYER_PARTIAL, out=self.P)
-            rs = self._reduce_scatter()
+            # push: item partial sums from this rank's users at layer k-1, chunk by chunk, each
+            # chunk's exchange issued as soon as its launch is queued
+            ex = []
+            for Ac, c0, m in self.push_chunks:
+                self.layer_fn(Ac, self.Xu[k - 1], _lib.LGX_LAYER_PARTIAL,
+                              out=self._chunk_views(c0, m)[0].view(s.world * m, self.d))
+                ex.append(self._exchange(c0, m))
+            if rec:
+                rec.mark("push")
             # pull: this rank's user rows from the full item table of layer k-1
             if ag is not None:
                 ag.wait()
+                if rec:
+                    rec.mark("allgather_wait")
             Xi = self.Xi[self._buf(k - 1)]
             if self.K == 1:
                 self.layer_fn(s.A_pull, Xi, _lib.LGX_LAYER_ONLY, E0=self.E0u, out=self.out_u, n_mean=n_mean)
@@ -280,15 +413,37 @@ class ShardedPropagation:
                 self.layer_fn(s.A_pull, Xi, _lib.LGX_LAYER_PLAIN, Y=self.Xu[k])
             else:
                 self.stack_fn(s.A_pull, Xi, self.E0u, self.Xu[1:self.K], self.out_u, n_mean)
-            # items: epilogue on the summed block, then publish it for the next pull
-            if rs is not None:
-                rs.wait()
+            if rec:
+                rec.mark("pull")
+            # items: the ordered cross-rank sums of the own block, its epilogue, then publish it
+            for (_, c0, m), h in zip(self.push_chunks, ex):
+                if h is not None:
+                    h.wait()
+                    if rec:
+                        rec.mark("exchange_wait")
+                self._reduce(c0, m)
+                if rec:
+                    rec.mark("reduce")
             n_i = s.n_i_local
             Yi = self.send_i[:n_i] if k < self.K else None
             self.epilogue_fn(self.yi[:n_i], mode, Y=Yi, E0=self.E0i, acc=self.acc_i, out=self.out_i,
                              n_mean=n_mean)
+            if rec:
+                rec.mark("epilogue")
             ag = self._all_gather(self.Xi[self._buf(k)]) if k < self.K else None
+        if rec:
+            rec.end()
         return self.out_u, self.out_i
+
+    def phase_summary(self) -> Dict[str, float]:
+        """Mean ms per recorded step by phase, plus comm_exposed_ms = allgather_wait +
+        exchange_wait (the stream's time behind collectives).  Synchronises the device."""
+        if self.phases.cuda:
+            torch.cuda.synchronize()
+        ph = self.phases.summary()
+        ph.pop("begin", None)
+        ph["comm_exposed_ms"] = ph.get("allgather_wait", 0.0) + ph.get("exchange_wait", 0.0)
+        return ph
 
     def gather_outputs(self) -> Tuple[torch.Tensor, torch.Tensor]:
         """All-gather the sharded layer means into full [U, d] / [I, d] fp32 tables."""

@@ -182,18 +182,47 @@ class CSRGraph:
 
     def col_block_count(self, d: int, elem_size: int) -> int:
         """Column blocks of the item rows for tables of d x elem_size-byte rows (0 = none): the
-        square bipartite operator only, when the user table they gather exceeds 1 GiB."""
+        square bipartite operator only, when the user table they gather is at least
+        ``col_block_min`` bytes (4 GiB), its plan phased users-first, and every item row holding
+        user columns only.  That last condition is what makes the item rows' (row, column) keys
+        sorted, which ``col_blocks`` relies on: an operator with self-loops (the reference TF
+        'norm' / plain adjacencies add the identity, load_data.py:142, LightGCN.py:457) keeps the
+        one-launch layer.  The checks run once per graph and the count once per table shape."""
         if not self.col_blocking or self.phases() is None or self.n_users < 2:
             return 0
         table = self.n_users * d * elem_size
         if table < self.col_block_min:
             return 0
+        key = ("cb_count", d, elem_size, self.col_block_min, self.col_block_slice)
+        got = self._dev_plan.get(key)
+        if got is not None:
+            return got
         self.ensure_plan()
-        p = self.plan
-        nu, ns = int(np.count_nonzero(p.seg_row < self.n_users)), int(np.count_nonzero(p.split_row < self.n_users))
-        if not ((p.seg_row[:nu] < self.n_users).all() and (p.split_row[:ns] < self.n_users).all()):
-            return 0  # a plan that is not phased users-first: keep the one-launch layer
-        return int(max(1, min(64, -(-table // self.col_block_slice), self.n_users)))
+        nb = 0
+        if self._users_first_plan() and self._item_rows_gather_users_only():
+            nb = int(max(1, min(64, -(-table // self.col_block_slice), self.n_users)))
+        self._dev_plan[key] = nb
+        return nb
+
+    def _users_first_plan(self) -> bool:
+        """The plan's user-row segments and split rows form a prefix (phases users, then items)."""
+        got = self._dev_plan.get("users_first")
+        if got is None:
+            p, U = self.plan, self.n_users
+            nu, ns = int(np.count_nonzero(p.seg_row < U)), int(np.count_nonzero(p.split_row < U))
+            got = bool((p.seg_row[:nu] < U).all() and (p.split_row[:ns] < U).all())
+            self._dev_plan["users_first"] = got
+        return got
+
+    def _item_rows_gather_users_only(self) -> bool:
+        """Every column of the item rows is a user id (< n_users), checked on the device."""
+        got = self._dev_plan.get("items_users_only")
+        if got is None:
+            s0 = int(self.indptr[self.n_users].item())
+            tail = self.indices[s0:]
+            got = bool(tail.numel() == 0 or int(tail.max().item()) < self.n_users)
+            self._dev_plan["items_users_only"] = got
+        return got
 
     def col_blocks(self, nb: int) -> dict:
         """Block b of item row r covers the nonzeros [ptr[b, r], ptr[b + 1, r]) -- the columns

@@ -72,6 +72,19 @@ def layer_epilogue(y: torch.Tensor, mode: int, Y: Optional[torch.Tensor] = None,
                "lgx_layer_epilogue")
 
 
+def sum_slabs(src: torch.Tensor, out: torch.Tensor) -> None:
+    """``lgx_sum_slabs``: out = src[0] + src[1] + ... + src[n-1], added in slab order in fp32
+    (src [n, rows, d] and out [rows, d], contiguous float32): the deterministic reduce step of the
+    sharded layer (distributed.py)."""
+    require_gpu(src, out)
+    if src.dtype != torch.float32 or out.dtype != torch.float32 or not (src.is_contiguous() and out.is_contiguous()):
+        raise ValueError("sum_slabs: contiguous float32 tensors")
+    if src.dim() < 2 or tuple(src.shape[1:]) != tuple(out.shape):
+        raise ValueError(f"sum_slabs: src {tuple(src.shape)} vs out {tuple(out.shape)}")
+    _lib.check(_lib.lib().lgx_sum_slabs(_ptr(src), src.shape[0], out.numel(), _ptr(out), _stream_ptr(out.device)),
+               "lgx_sum_slabs")
+
+
 def spmm(A: CSRGraph, X: torch.Tensor) -> torch.Tensor:
     """Y = A X (the reference's ``torch.sparse.mm(G, all_emb)``, model.py:171)."""
     require_gpu(X)

@@ -27,6 +27,9 @@ import torch
 
 from . import ops
 
+# pinned staging slots of stratified_candidates' per-batch device-to-host copies
+_STAGE = 3
+
 
 def candidate_scores(emb_user: torch.Tensor, emb_item: torch.Tensor,
                      candidates: Sequence[Sequence[int]]) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
@@ -254,7 +257,8 @@ class CandidateLists(Sequence):
 
 def stratified_candidates(emb_user: torch.Tensor, emb_item: torch.Tensor, train, targets: Sequence[int],
                           num_fold: int = 10, epsilon: float = 0.1, seed: int = 0, batch: int = 4096,
-                          fused: Optional[bool] = None) -> CandidateLists:
+                          fused: Optional[bool] = None,
+                          bounds: Optional[Tuple[float, float]] = None) -> CandidateLists:
     """Per user, the stratified candidate list of create_candidates_stratification_sub +
     sample_list (recommend.py:314-356): labels and counts by strat_labels (fused into the scoring
     kernel's epilogue where the shape allows), the per-label random picks by lgx_strat_select.
@@ -262,8 +266,12 @@ def stratified_candidates(emb_user: torch.Tensor, emb_item: torch.Tensor, train,
     ``train`` is a list of per-user train item lists, or a (indptr, indices) CSR pair.  Raises
     ValueError where the reference's sampling raises: a negative target (DataFrame.sample(n < 0))
     or a list that sample_list cannot pad to its target (random.sample(lst, k > len(lst)),
-    recommend.py:317).  The per-batch picks are copied into one pinned host array while the GPU
-    works on the next batch; rows become lists only when read (CandidateLists)."""
+    recommend.py:317).  ``bounds`` = (min_dis, inter16) when the label grid comes from more users
+    than are labelled here (the reference's np.max / np.min run over the whole emb_user @ emb_item.T,
+    recommend.py:375-377); by default they come from emb_user itself.  Each batch's picks go through
+    a small ring of pinned staging buffers into one pageable host array, the copy of batch b
+    overlapping the GPU work of the next batches; rows become lists only when read
+    (CandidateLists)."""
     from . import _lib
     dev = torch.device(emb_user.device)
     ops.require_gpu(emb_user, emb_item)
@@ -277,7 +285,10 @@ def stratified_candidates(emb_user: torch.Tensor, emb_item: torch.Tensor, train,
     if U and tgt_h.max() > 1024:
         raise ValueError("at most 1024 candidates per user")
     with torch.cuda.device(dev):
-        min16, inter16 = stratification_bounds(emb_user, emb_item, num_fold, epsilon)
+        if bounds is None:
+            min16, inter16 = stratification_bounds(emb_user, emb_item, num_fold, epsilon)
+        else:
+            min16, inter16 = (float(x) for x in bounds)
         if isinstance(train, tuple):
             mp, mi = (t.to(dev) for t in train)
             mi = mi.to(torch.int32)
@@ -290,9 +301,24 @@ def stratified_candidates(emb_user: torch.Tensor, emb_item: torch.Tensor, train,
         L = _lib.lib()
         stream = torch.cuda.current_stream(dev)
         st = ops._stream_ptr(dev)
-        picks = torch.empty((U, K), dtype=torch.int32, pin_memory=True)
-        counts = torch.empty(U, dtype=torch.int32, pin_memory=True)
-        for b0 in range(0, U, batch):
+        picks = np.empty((U, K), dtype=np.int32)
+        counts = np.empty(U, dtype=np.int32)
+        # pinned staging: a ring of _STAGE batch slots (not U x K pinned bytes: 4 GB at 1 M users x
+        # 1000 candidates, slow to page-lock); slot j is drained into the pageable arrays once the
+        # copy that last filled it has completed
+        nring = min(_STAGE, -(-U // batch)) if U else 0
+        ring = [(torch.empty((batch, K), dtype=torch.int32, pin_memory=True),
+                 torch.empty(batch, dtype=torch.int32, pin_memory=True)) for _ in range(nring)]
+        pending = [None] * nring  # (event, b0, b1) of the copy in flight into each slot
+
+        def drain(j):
+            ev, c0, c1 = pending[j]
+            ev.synchronize()
+            picks[c0:c1] = ring[j][0][:c1 - c0].numpy()
+            counts[c0:c1] = ring[j][1][:c1 - c0].numpy()
+            pending[j] = None
+
+        for bi, b0 in enumerate(range(0, U, batch)):
             b1 = min(U, b0 + batch)
             labels, hist = strat_labels(emb_user[b0:b1], emb_item, mp[b0:], mi, min16, inter16, num_fold, fused)
             out = torch.empty((b1 - b0, K), dtype=torch.int32, device=dev)
@@ -303,12 +329,18 @@ def stratified_candidates(emb_user: torch.Tensor, emb_item: torch.Tensor, train,
                                           out.data_ptr(), K, cnt.data_ptr(), st), "lgx_strat_select")
             # async D2H on the stream the kernels ran on: the copy engine drains batch b while the
             # next batch's labels run (the allocator keeps `out` alive until the copy is done)
-            picks[b0:b1].copy_(out, non_blocking=True)
-            counts[b0:b1].copy_(cnt, non_blocking=True)
-        done = torch.cuda.Event()
-        done.record(stream)
-    done.synchronize()
-    res = CandidateLists(picks.numpy(), counts.numpy())
+            j = bi % nring
+            if pending[j] is not None:
+                drain(j)
+            ring[j][0][:b1 - b0].copy_(out, non_blocking=True)
+            ring[j][1][:b1 - b0].copy_(cnt, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            pending[j] = (ev, b0, b1)
+        for j in range(nring):
+            if pending[j] is not None:
+                drain(j)
+    res = CandidateLists(picks, counts)
     short = np.flatnonzero(res.counts < tgt_h)
     if short.size:
         u = int(short[0])
@@ -320,6 +352,13 @@ def stratified_candidates(emb_user: torch.Tensor, emb_item: torch.Tensor, train,
 def train_csr(dataset_name: str, n_users: int, data_root: str = "data") -> Tuple[torch.Tensor, torch.Tensor]:
     """rating_train.csv as a sorted, de-duplicated CSR: row j = the j-th userInd group, as the
     reference zips mat_label with df_train.groupby("userInd") (recommend.py:372,421-422)."""
+    indptr, items, _ = train_groups(dataset_name, n_users, data_root)
+    return indptr, items
+
+
+def train_groups(dataset_name: str, n_users: int, data_root: str = "data"):
+    """train_csr plus the group keys: users[j] = the userInd of group j (sorted, groupby order),
+    the ``uind`` the reference pairs with row j of mat_label (recommend.py:421)."""
     import pandas as pd
     df = pd.read_csv(os.path.join(data_root, dataset_name, "rating_train.csv"), usecols=["userInd", "itemInd"])
     u = df["userInd"].to_numpy(np.int64)
@@ -331,7 +370,7 @@ def train_csr(dataset_name: str, n_users: int, data_root: str = "data") -> Tuple
     indptr = np.zeros(len(lens) + 1, np.int64)
     np.cumsum(lens, out=indptr[1:])
     items = (key[:indptr[-1]] & 0xFFFFFFFF).astype(np.int32)
-    return torch.from_numpy(indptr), torch.from_numpy(items)
+    return torch.from_numpy(indptr), torch.from_numpy(items), users[:len(lens)]
 
 
 class CandidateDict(Mapping):
@@ -397,12 +436,18 @@ def create_candidates_stratification(dataset_name: str, seed: int, K_c: int = 10
     test = pd.read_csv(os.path.join(data_root, dataset_name, "rating_test.csv")) \
         .groupby("userInd")["itemInd"].apply(list).to_dict()
     if not os.path.exists(path_list_res):
-        train = train_csr(dataset_name, emb_user.shape[0], data_root)
-        n = train[0].numel() - 1
-        targets = [K_c - len(test[u]) for u in range(n)]             # KeyError as at :426
-        eu = torch.from_numpy(np.ascontiguousarray(emb_user[:n], dtype=np.float32)).to(device)
+        indptr, items, uinds = train_groups(dataset_name, emb_user.shape[0], data_root)
+        n = indptr.numel() - 1
+        # zip(mat_label, group_train): row j of the labels (user j) with the j-th group, whose key
+        # uind picks the test list that sets the target (recommend.py:421,426)
+        targets = [K_c - len(test[int(u)]) for u in uinds]           # KeyError as at :426
+        eu = torch.from_numpy(np.ascontiguousarray(emb_user, dtype=np.float32)).to(device)
         ei = torch.from_numpy(np.ascontiguousarray(emb_item, dtype=np.float32)).to(device)
-        list_res = stratified_candidates(eu, ei, train, targets, num_fold, epsilon, seed)
+        # the label grid spans the whole emb_user @ emb_item.T (recommend.py:375-377), also when
+        # fewer train groups than users are labelled
+        bounds = stratification_bounds(eu, ei, num_fold, epsilon)
+        list_res = stratified_candidates(eu[:n], ei, (indptr, items), targets, num_fold, epsilon, seed,
+                                         bounds=bounds)
         os.makedirs(out_dir, exist_ok=True)
         with open(path_list_res, "wb") as f:
             pickle.dump(list_res, f)

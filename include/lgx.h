@@ -117,7 +117,8 @@ typedef struct lgx_csr {
      * cb_n > 0: the plan above covers rows [0, cb_row0) only, and the blocked rows run as cb_n
      * launches, block b over the nonzeros [cb_ptr[b R + r], cb_ptr[(b + 1) R + r]) of row
      * cb_row0 + r (R = n_rows - cb_row0; columns ascending, so a block is one range of columns and
-     * its gathers stay inside one slice of the table, small enough for the MALL), each with its
+     * its gathers stay inside one 1/cb_n slice of the table: 640 MiB at C4 f32, larger than the
+     * 256 MiB MALL, but a narrower working set that measured 57.2 -> 53.6 ms per layer), each with its
      * own plan cb_plans[b] (host array; seg_row holds global rows).  Row sums are carried between
      * the block launches in cb_carry [R, d] f32; the last block adds them and runs the epilogue.
      */
@@ -172,6 +173,15 @@ int lgx_propagate_layer(const lgx_csr* A, const void* X, void* Y, const void* E0
  */
 int lgx_layer_epilogue(const float* y, int64_t rows, void* Y, const void* E0, float* acc, float* out,
                        int64_t d, int dtype, int mode, float n_mean, lgx_stream_t stream);
+/*
+ * Cross-rank sum of LGX_LAYER_PARTIAL outputs after their exchange (the sharded layer's
+ * reduce step): dst[i] = src[0 * slab_elems + i] + src[1 * slab_elems + i] + ... + src[(n_slabs-1) *
+ * slab_elems + i], added in slab order in fp32, so the result is independent of how the exchange
+ * was chunked and of the collective's own reduction order.  slab_elems a multiple of 4, src / dst
+ * 16-B aligned, dst may not overlap src.  Replaces the reference's concat of per-fold SpMM
+ * outputs (dataloader.py:319-329, model.py:164-168) on the multi-GPU path.
+ */
+int lgx_sum_slabs(const float* src, int64_t n_slabs, int64_t slab_elems, float* dst, lgx_stream_t stream);
 /*
  * Host-only introspection: the name of the SpMM kernel instantiation lgx_propagate_layer launches
  * for (d, dtype, plan seg_len), e.g. "spmm_segments<bf16,16,1,16>".  Lets tests pin the exact

@@ -98,6 +98,60 @@ def test_sharded_propagation_gloo(world, K):
     assert len(sched) == 3 * K
 
 
+def _chunk_worker(rank, world, port, K, result_q):
+    """One graph, the same shard, propagated with 1 / 3 / 4 / 7 push chunks: gathered outputs equal
+    bit for bit (each row keeps its summation; the cross-rank sum runs in rank order); phases
+    recorded for every step."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(7)
+        U, I, E = 150, 97, 3000
+        u = rng.integers(0, U, E).astype(np.int32)
+        i = (rng.zipf(1.3, E) % I).astype(np.int32)
+        ip, ix, iv = oracle.build_norm_adj(u, i, U, I, dedup=True)
+        A = CSRGraph(torch.from_numpy(ip), torch.from_numpy(ix), torch.from_numpy(iv), U + I, U + I, U, I)
+        E0 = torch.from_numpy((rng.standard_normal((U + I, 8)) * 0.1).astype(np.float32))
+        shard = make_shard(A, U, I, rank, world, seg_len=16)
+        outs, phases = [], None
+        for nc in (1, 3, 4, 7):
+            prop = ShardedPropagation(shard, E0[:U], E0[U:], K, layer_fn=cpu_layer, epilogue_fn=cpu_epilogue,
+                                      stack_fn=cpu_stack, n_chunks=nc)
+            assert len(prop.push_chunks) == min(nc, shard.mi)
+            prop.record_phases = nc == 4
+            prop.step()
+            prop.step()
+            if nc == 4:
+                phases = prop.phase_summary()
+            ou, oi = prop.gather_outputs()
+            outs.append(torch.cat([ou, oi]).numpy())
+        if rank == 0:
+            ref = oracle.propagate(ip, ix, iv, E0.numpy(), K)
+            result_q.put(([bool(np.array_equal(outs[0], o)) for o in outs[1:]],
+                          float(np.abs(outs[0] - ref).max()), phases))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_chunked_exchange_equals_unchunked_bit_for_bit(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_chunk_worker, args=(r, world, port, 3, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    same, err, phases = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert all(same), same
+    assert err < 1e-5
+    for name in ("push", "allgather_wait", "pull", "exchange_wait", "reduce", "epilogue", "comm_exposed_ms"):
+        assert name in phases and phases[name] >= 0.0, phases
+
+
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
 def test_shard_from_edges_equals_cut_of_full_operator(world):
     """make_shard_from_edges (each rank builds only its rows from the sorted edge list) == make_shard

@@ -58,3 +58,30 @@ def test_column_blocked_propagation(nb, dtype, K):
     Yr = oracle.spmm(ip, ix, iv, E0)
     assert np.allclose(Y, Yr, rtol=1e-5 if dtype == torch.float32 else 2e-2,
                        atol=(1e-6 if dtype == torch.float32 else 2e-2) * np.abs(Yr).max())
+
+
+def test_self_loop_operator_is_not_column_blocked():
+    """An operator with self-loops (the reference's TF 'norm' adjacency D^-1 (A + I),
+    load_data.py:142, or A + I wrapped through from_csr_arrays) has item rows holding an item
+    column, so their (row, column) keys are not sorted by user block: col_block_count must refuse
+    it even when the table size asks for blocks, and the layer still equals the oracle."""
+    import scipy.sparse as sp
+    ip, ix, iv, U, I = _graph(7)
+    N = U + I
+    M = (sp.csr_matrix((iv, ix, ip), shape=(N, N)) + sp.identity(N, dtype=np.float32, format="csr")).tocsr()
+    M.sort_indices()
+    ip2, ix2, iv2 = M.indptr.astype(np.int64), M.indices.astype(np.int32), M.data.astype(np.float32)
+    d = 64
+    A = lgx.from_csr_arrays(ip2, ix2, iv2, device=DEV, n_users=U, n_items=I, seg_len=8)
+    A.col_block_min = 1
+    A.col_block_slice = -(-U * d * 4 // 4)
+    assert A.col_block_count(d, 4) == 0
+    # the same graph without the loops does block at these settings
+    B = lgx.from_csr_arrays(ip, ix, iv, device=DEV, n_users=U, n_items=I, seg_len=8)
+    B.col_block_min, B.col_block_slice = 1, A.col_block_slice
+    assert B.col_block_count(d, 4) == 4
+    rng = np.random.default_rng(3)
+    E0 = (rng.standard_normal((N, d)) * 0.1).astype(np.float32)
+    out = lgx.propagate(A, torch.from_numpy(E0).to(DEV), 3).cpu().numpy()
+    ref = oracle.propagate(ip2, ix2, iv2, E0, 3)
+    assert (np.abs(out - ref) <= 1e-5 * np.abs(ref) + 1e-6 * np.abs(E0).max()).all()

@@ -46,14 +46,21 @@ def _worker(rank, world, port, K, dtype_name, q, backend="gloo"):
         if dtype == torch.bfloat16:
             E0 = E0.to(torch.bfloat16).float()
         shard = make_shard(A, U, I, rank, world, seg_len=64)
-        prop = ShardedPropagation(shard, E0[:U].cuda().to(dtype), E0[U:].cuda().to(dtype), K,
-                                  force_collectives=backend == "nccl")
-        if backend == "nccl":
-            assert prop._collective and prop._rs_native  # async reduce_scatter_tensor / all_gather_into_tensor
-        prop.step()
-        prop.step()
-        ou, oi = prop.gather_outputs()
+        outs = []
+        for nc in (1, 4):  # one push launch, then 4 chunks each with its own exchange
+            prop = ShardedPropagation(shard, E0[:U].cuda().to(dtype), E0[U:].cuda().to(dtype), K,
+                                      force_collectives=backend == "nccl", n_chunks=nc)
+            if backend == "nccl":
+                assert prop._collective and prop._a2a_native  # async all_to_all_single / all_gather_into_tensor
+            prop.record_phases = True
+            prop.step()
+            prop.step()
+            ph = prop.phase_summary()
+            assert ph["push"] > 0 and ph["pull"] > 0 and ph["comm_exposed_ms"] >= 0, ph
+            ou, oi = prop.gather_outputs()
+            outs.append((ou.clone(), oi.clone()))
         torch.cuda.synchronize()
+        assert all(torch.equal(a, b) for a, b in zip(outs[0], outs[1])), "chunked layer differs from one launch"
         if rank == 0:
             ref = oracle.propagate(A.indptr.cpu().numpy(), A.indices.cpu().numpy(), A.vals.cpu().numpy(),
                                    E0.numpy(), K)

@@ -121,6 +121,47 @@ def test_create_candidates_stratification_dropin(tmp_path):
     assert os.path.exists(root / "s" / "rec" / "3" / "candidate.npy")
 
 
+def test_create_candidates_groups_targets_and_bounds(tmp_path, monkeypatch):
+    """Train user ids that are not dense 0..n-1 and more emb_user rows than train groups: the
+    reference zips mat_label row j (user j) with the j-th train group, takes the target from the
+    group key's test list (recommend.py:421,426), appends the test list of position j (:450), and
+    its label grid spans every emb_user row (np.max / np.min of the full product, :375-377)."""
+    import pandas as pd
+    U, I, K_c = 30, 2000, 300
+    eu, ei, train = _setup(4, U=U, I=I)
+    eu[U - 1] *= 6.0  # the last user (no train group) holds the extreme scores
+    rng = np.random.default_rng(10)
+    test = [rng.choice(I, int(rng.integers(1, 6)), replace=False).tolist() for _ in range(U)]
+    groups = [u for u in range(U - 1) if u != 4]  # user 4 and the last user have no train rows
+    root = tmp_path / "data"
+    (root / "s").mkdir(parents=True)
+    np.save(root / "s" / "emb_user.npy", eu)
+    np.save(root / "s" / "emb_item.npy", ei)
+    pd.DataFrame([(u, i) for u in groups for i in train[u]], columns=["userInd", "itemInd"]) \
+        .to_csv(root / "s" / "rating_train.csv", index=False)
+    pd.DataFrame([(u, i) for u, l in enumerate(test) for i in l], columns=["userInd", "itemInd"]) \
+        .to_csv(root / "s" / "rating_test.csv", index=False)
+    seen = {}
+    real = recommend.stratified_candidates
+
+    def spy(*args, **kw):
+        seen["bounds"] = kw.get("bounds")
+        seen["n"] = args[0].shape[0]
+        return real(*args, **kw)
+
+    monkeypatch.setattr(recommend, "stratified_candidates", spy)
+    cand = recommend.create_candidates_stratification("s", 3, K_c=K_c, data_root=str(root), device=DEV)
+    full = recommend.stratification_bounds(torch.from_numpy(eu).to(DEV), torch.from_numpy(ei).to(DEV), 10, 0.1)
+    sub = recommend.stratification_bounds(torch.from_numpy(eu[:len(groups)]).to(DEV), torch.from_numpy(ei).to(DEV),
+                                          10, 0.1)
+    assert seen["n"] == len(groups) and seen["bounds"] == full and full != sub
+    assert sorted(cand) == list(range(len(groups)))
+    for j, g in enumerate(groups):
+        assert len(cand[j]) == K_c - len(test[g]) + len(test[j]), j
+        assert cand[j][len(cand[j]) - len(test[j]):] == test[j]
+        assert not np.isin(cand[j][:K_c - len(test[g])], train[g]).any()
+
+
 def test_fast_select_equals_radix_select():
     """the cut-and-rank fast path picks exactly the sets (and order) of the exact radix select:
     long rows (fast path taken), a tiny label (cut = everything), and a row whose candidates

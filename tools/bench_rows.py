@@ -111,24 +111,44 @@ def row_a2(rows, reps):
 
 # ------------------------------------------------------------------------------------- a6 + a9
 def row_a6_a9(rows, reps):
-    """getUsersRating [B, I] (model.py:179-184) and the row top-K of tools.h:13-33 on it."""
+    """getUsersRating [B, I] = sigmoid(E_u[users] E_i^T) (model.py:179-184) and the row top-K of
+    tools.h:13-33 on it: bf16 [4096, 1M] d=256 (SURVEY C5 inputs; write-bound), then the reference's
+    fp32 at its own test batch (B=100, parse.py:26) and at [4096, 1M] (both f32-MFMA-bound)."""
     B, I, d, k = 4096, 1_000_000, 256, 20
     Q = ops.fill_normal((B, d), 1.0 / 16, 1, dtype=torch.bfloat16)
     items = ops.fill_normal((I, d), 1.0 / 16, 2, dtype=torch.bfloat16)
-    S = ops.score_dense(Q, items)
-    ms = gpu_ms(lambda: ops.score_dense(Q, items), reps)
+    S = ops.score_dense(Q, items, apply_sigmoid=True)
+    ms = gpu_ms(lambda: ops.score_dense(Q, items, apply_sigmoid=True), reps)
+    ms_raw = gpu_ms(lambda: ops.score_dense(Q, items), reps)
     Qc, Ic = Q[:64].float().cpu(), items.float().cpu()
     torch.set_num_threads(CPU_THREADS)
     s = cpu_s(lambda: torch.sigmoid(torch.matmul(Qc, Ic.t())))
-    emit(rows, "a6 dense scoring (lgx_score_dense)", ms, B * I, "scores/s", "hbm", 4 * B * I + 2 * I * d + 2 * B * d,
-         64 * I, s, f"64 users x {I} items, d={d} fp32 torch.matmul + sigmoid", CPU_THREADS,
-         f"bf16 in, f32 out [B, I]; flops {2 * B * I * d:.3g} (MFMA well under its roof: write-bound)")
+    emit(rows, "a6 dense scoring, bf16 (lgx_score_dense, sigmoid)", ms, B * I, "scores/s", "hbm",
+         4 * B * I + 2 * I * d + 2 * B * d, 64 * I, s, f"64 users x {I} items, d={d} fp32 torch.matmul + sigmoid",
+         CPU_THREADS, f"bf16 in, f32 out [B, I]; flops {2 * B * I * d:.3g} (MFMA well under its roof: write-bound); "
+                      f"raw scores (TF batch_ratings, no sigmoid) {ms_raw:.2f} ms")
     ms = gpu_ms(lambda: ops.topk_rows(S, k), reps)
     Sc = S[:256].cpu()
     s = cpu_s(lambda: torch.topk(Sc, k))
     emit(rows, "a9 row top-K (lgx_topk_rows)", ms, B * I, "scores/s", "hbm", 4 * B * I + 8 * B * k,
          256 * I, s, f"256 rows x {I} torch.topk(k={k})", CPU_THREADS)
     del S, Q, items
+    torch.cuda.empty_cache()
+    # the reference's precision: fp32 tables, fp32 products (model.py:183)
+    items = ops.fill_normal((I, d), 1.0 / 16, 2)
+    Ic = items.cpu()
+    for Bf in (100, 4096):
+        Q = ops.fill_normal((Bf, d), 1.0 / 16, 3)
+        ms = gpu_ms(lambda: ops.score_dense(Q, items, apply_sigmoid=True), reps)
+        nc = min(Bf, 64)
+        Qc = Q[:nc].cpu()
+        s = cpu_s(lambda: torch.sigmoid(torch.matmul(Qc, Ic.t())))
+        emit(rows, f"a6 dense scoring, fp32 B={Bf} (lgx_score_dense, sigmoid)", ms, Bf * I, "scores/s", "mfma_f32",
+             2.0 * Bf * I * d, nc * I, s, f"{nc} users x {I} items, d={d} fp32 torch.matmul + sigmoid", CPU_THREADS,
+             f"f32 in, f32 out [{Bf}, {I}] ({4 * Bf * I / 1e9:.2f} GB written: "
+             f"{4 * Bf * I / HBM_PEAK * 1e3:.3f} ms at the HBM peak) -- bound by the f32 MFMA flops")
+        del Q
+    del items
     torch.cuda.empty_cache()
 
 

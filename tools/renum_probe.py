@@ -1,7 +1,7 @@
 """Development probe: does a degree-ordered numbering of the C4 graph (users and items each sorted by
 descending degree) change the SpMM layer time, alone and with non-temporal cold gathers?
 
-  python tools/renum_probe.py [--lib tools/liblgx_ntcold.so --cuts 16384:131072,65536:262144]
+  python tools/renum_probe.py
 
 Times the fused MID layer (bf16 d=128) on the original and the renumbered graph; with the ntcold
 library, also with gathers of users ranked >= Hu and items ranked >= Hi non-temporal (H pairs
@@ -19,7 +19,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 ap = argparse.ArgumentParser()
 ap.add_argument("--lib", default=None)
-ap.add_argument("--cuts", default="")
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--dtype", default="bf16")
 args = ap.parse_args()
@@ -85,13 +84,4 @@ torch.cuda.empty_cache()
 B = lgx.from_csr_arrays(indptr, ncol, vals, device="cuda", n_users=U, n_items=I)
 print(f"renumbered in {time.time() - t0:.1f}s", flush=True)
 print(f"degree-ordered        MID {layer(B):8.3f} ms", flush=True)
-L = _lib.lib()
-if args.cuts:
-    f = L.lgx_dev_set_nt_cut
-    f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
-    for c in args.cuts.split(","):
-        hu, hi = (int(x) for x in c.split(":"))
-        f(hu, U, U + hi)
-        print(f"degree-ordered nt cold users>={hu} items>={hi}  MID {layer(B):8.3f} ms", flush=True)
-    f(0x7fffffff, 0x7fffffff, 0x7fffffff)
 print("probe done", flush=True)

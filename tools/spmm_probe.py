@@ -1,6 +1,6 @@
 """Development probe: where the C4 SpMM layer spends its time (not part of the library).
 
-  python tools/spmm_probe.py [--lib tools/liblgx_nt.so] [--blocks 8,16]
+  python tools/spmm_probe.py [--blocks 8,16]
 
 Builds the synth10m graph (10M users x 1M items, 1e9 nnz, d=128 bf16) and times, with HIP events:
   * the full fused layer (MID mode), as the bench runs it;
