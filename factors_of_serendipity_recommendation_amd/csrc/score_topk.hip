@@ -698,6 +698,52 @@ constexpr int kMinMaxOnly = 1;
 // it, and a sweep that starts its lists with this threshold drops no item of the exact top-k (ties
 // at the floor included: a filling list takes scores >= floor).  A product mode.
 constexpr int kFloorOnly = 2;
+// The fp32 walk's dense modes (lgx_score_dense and lgx_strat_labels_fused in fp32, d a multiple of
+// 64): every score of the tile leaves the accumulators -- as an f32 score (kDenseScores, with the
+// reference's sigmoid under kDenseSigmoid, model.py:183) or as the stratification label of
+// recommend.py:375-381 with its per-user counts (kStratLabels).  One walk (items the A operand from
+// the LDS ring, users the B operand in registers, the same k order) gives both the same f32 sums,
+// so the fused labels equal the labels of the dense scores bit for bit.
+constexpr int kDenseScores = 3;
+constexpr int kDenseSigmoid = 4;
+constexpr int kStratLabels = 5;
+__host__ __device__ constexpr bool dense_mode(int m) { return m == kDenseScores || m == kDenseSigmoid || m == kStratLabels; }
+
+struct StratThr {
+    float t[32];
+    int n;
+    float base, inv;  // estimate: floor((s - base) * inv) is the label within +-1 (thresholds ~ evenly spaced)
+};
+
+// the label of score sc: the count of thresholds it reaches (recommend.py:379-381 restated on the f32
+// score, lgx_strat_thresholds).  T[j] = the score where label j starts (T[0] = -inf, T[n + 1] =
+// +inf), TP[j] = {T[j], T[j + 1]}.  EST1: the host proved the estimate within one of the label, so
+// one branch-free step each way corrects it; otherwise an exact walk from the estimate.
+template <bool EST1>
+__device__ __forceinline__ uint32_t strat_label_of(float sc, const StratThr& thr, const float* T, const float2* TP) {
+    const float x = (sc - thr.base) * thr.inv;
+    int l = (x >= (float)thr.n || x != x) ? thr.n : (x < 0.0f ? 0 : (int)x);  // NaN -> n, as label_of
+    if (EST1) {
+        const float2 tp = TP[l];  // T[l], T[l + 1]
+        return (uint32_t)(l - (sc < tp.x && l > 0 ? 1 : 0) + (sc >= tp.y && l < thr.n ? 1 : 0));
+    }
+    while (l > 0 && sc < T[l]) --l;
+    while (l < thr.n && sc >= T[l + 1]) ++l;
+    return (uint32_t)l;
+}
+
+// outputs of the dense modes
+struct WalkOut {
+    float* scores;   // kDenseScores / kDenseSigmoid: [B, n_items] f32
+    int8_t* labels;  // kStratLabels: [B, n_items] int8
+    int32_t* hist;   // kStratLabels: [B, thr.n + 1] label counts (added to), or nullptr
+    StratThr thr;
+    int vec4;        // n_items % 4 == 0 and 16-B aligned rows: one 16-B / 4-B store per 4 items
+    int est1;        // kStratLabels: the label estimate is within one of the label (host-proved)
+};
+// label counts of the workgroup's users in LDS, stride 17: the 16 users of a lane group sit in 16
+// different banks
+constexpr int kHistStride = 17;
 
 template <int KSTEPS, int WAVES = 8, int NACC = 2, int ESZ = 2>
 struct LdsGeom {
@@ -776,9 +822,10 @@ constexpr int kBf16LdsWaves = 8;
 constexpr int kF32LdsWaves = 4;
 template <int DT, int KSTEPS, bool MINMAX, int MODE, int WAVES, int NACC, bool STAGGER>
 __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreArgs a, int xcd_affine,
-                                                    int64_t n_utiles, int nbuf) {
+                                                    int64_t n_utiles, int nbuf, const WalkOut& o = WalkOut{}) {
     constexpr bool F32 = DT == LGX_DTYPE_F32;
     static_assert(NACC == 2 && (F32 || KSTEPS % 2 == 0), "16x16 walk: 64-item tiles, bf16 d a multiple of 32");
+    static_assert(!dense_mode(MODE) || (F32 && !STAGGER && !MINMAX), "dense modes: the fp32 walk");
     // SKIP: the fast-path test runs on the MFMA output layout itself (lane l holds 16 scores of user
     // l & 15 and 16 of user 16 + (l & 15)); the regroup into the top-k layout (16 v_permlane16_swap)
     // is paid only by tiles that have a survivor.  Min / max needs every score: not with MINMAX.
@@ -814,6 +861,17 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     const bool user_ok = b < a.B;
     uint4 uf[UFN];
     const int r16 = lane & 15, q4 = lane >> 4;
+    // kStratLabels: the per-user label counts and the thresholds, in LDS after the ring (published by
+    // the prologue's barrier)
+    uint32_t* hc = reinterpret_cast<uint32_t*>(smem + (size_t)nbuf * G::TILE);
+    float2* TP = reinterpret_cast<float2*>(hc + G::USERS * kHistStride);
+    float* T = reinterpret_cast<float*>(TP + 34);
+    if constexpr (MODE == kStratLabels) {
+        for (int e = threadIdx.x; e < G::USERS * kHistStride; e += WAVES * 64) hc[e] = 0u;
+        auto thr_at = [&](int j) { return j == 0 ? -INFINITY : (j <= o.thr.n ? o.thr.t[j - 1] : INFINITY); };
+        if (threadIdx.x < 34) T[threadIdx.x] = thr_at(threadIdx.x);
+        if (threadIdx.x < 33) TP[threadIdx.x] = make_float2(thr_at(threadIdx.x), thr_at(threadIdx.x + 1));
+    }
     // B fragment (ub, s) at uf[ub * NS + s]: user 16 ub + r16, 16-B chunk 4 s + q4 of its row
 #pragma unroll
     for (int ub = 0; ub < 2; ++ub) {
@@ -889,7 +947,10 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(ahead, ntiles) - 1));
     __syncthreads();
     int buf = 0, sbuf = ahead;  // buffer of tile t / of tile t + ahead
-    const bool late = STAGGER && MODE != kMinMaxOnly && wave >= WAVES / 2;  // wave-uniform
+    // dense modes: every wave writes a tile's scores after the barrier that follows its MFMAs, so the
+    // stores are younger than the next refill and have a tile of MFMAs to drain before the next
+    // vmcnt wait (which would otherwise wait for them)
+    const bool late = (STAGGER && MODE != kMinMaxOnly && wave >= WAVES / 2) || dense_mode(MODE);  // wave-uniform
     f32x16 acc0, acc1;  // late waves: tile t-1's scores, held across the barrier
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     f32x4 c[2][4];      // 16x16x32 accumulators: c[ub][ib] = items 16 ib + 4 (lane >> 4) + reg, user 16 ub + (lane & 15)
@@ -1019,7 +1080,72 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
                 gm[1][ib][r] = in ? fmaxf(gm[1][ib][r], c[1][ib][r]) : gm[1][ib][r];
             }
     };
+    // dense modes: lane (q4, r16) holds items e0 + 16 ib + 4 q4 + 0..3 of user 16 ub + r16
+    auto dense_tile = [&](int64_t e0) {
+        const int64_t rem = i_end - e0;  // items of the tile inside the split
+#pragma unroll
+        for (int ub = 0; ub < 2; ++ub) {
+            const int64_t bu = utile * G::USERS + wave * kUsersPerWave + 16 * ub + r16;
+            if (bu >= a.B) continue;
+            float* row = o.scores + bu * a.n_items + e0;
+#pragma unroll
+            for (int ib = 0; ib < 4; ++ib) {
+                const int off = 16 * ib + 4 * q4;
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    v[r] = MODE == kDenseSigmoid ? 1.0f / (1.0f + expf(-c[ub][ib][r])) : c[ub][ib][r];
+                if (o.vec4 && off + 4 <= rem) {
+                    *reinterpret_cast<float4*>(row + off) = make_float4(v[0], v[1], v[2], v[3]);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (off + r < rem) row[off + r] = v[r];
+                }
+            }
+        }
+    };
+    auto label_tile = [&](auto est_tag, int64_t e0) {
+        constexpr bool EST1 = decltype(est_tag)::value;
+        const int64_t rem = i_end - e0;
+#pragma unroll
+        for (int ub = 0; ub < 2; ++ub) {
+            const int64_t bu = utile * G::USERS + wave * kUsersPerWave + 16 * ub + r16;
+            if (bu >= a.B) continue;
+            int8_t* row = o.labels + bu * a.n_items + e0;
+            uint32_t* hu = hc + (wave * kUsersPerWave + 16 * ub + r16) * kHistStride;
+#pragma unroll
+            for (int ib = 0; ib < 4; ++ib) {
+                const int off = 16 * ib + 4 * q4;
+                uint32_t l[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) l[r] = strat_label_of<EST1>(c[ub][ib][r], o.thr, T, TP);
+                if (o.hist) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (off + r < rem) atomicAdd(hu + l[r], 1u);
+                }
+                const uint32_t w = l[0] | (l[1] << 8) | (l[2] << 16) | (l[3] << 24);
+                if (o.vec4 && off + 4 <= rem) {
+                    *reinterpret_cast<uint32_t*>(row + off) = w;
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (off + r < rem) row[off + r] = (int8_t)((w >> (8 * r)) & 255);
+                }
+            }
+        }
+    };
     auto epilogue = [&](int64_t e0) {
+        if constexpr (MODE == kDenseScores || MODE == kDenseSigmoid) {
+            dense_tile(e0);
+            return;
+        }
+        if constexpr (MODE == kStratLabels) {
+            if (o.est1) label_tile(std::true_type{}, e0);
+            else label_tile(std::false_type{}, e0);
+            return;
+        }
         if constexpr (MODE == kMinMaxOnly) {
             minmax_tile();
             return;
@@ -1099,6 +1225,19 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         sbuf = sbuf + 1 == nbuf ? 0 : sbuf + 1;
     }
     if (late && ntiles > 0) epilogue(prev_t0);
+    if constexpr (MODE == kStratLabels) {  // the workgroup's counts into the global histogram
+        __syncthreads();
+        if (o.hist) {
+            const int64_t u0 = utile * G::USERS;
+            for (int e = threadIdx.x; e < G::USERS * kHistStride; e += WAVES * 64) {
+                const int uu = e / kHistStride, l = e % kHistStride;
+                const uint32_t cnt = hc[e];
+                if (cnt && l <= o.thr.n && u0 + uu < a.B) atomicAdd(o.hist + (u0 + uu) * (o.thr.n + 1) + l, (int32_t)cnt);
+            }
+        }
+        return;
+    }
+    if constexpr (MODE == kDenseScores || MODE == kDenseSigmoid) return;
     if constexpr (MODE == kMinMaxOnly) {
 #pragma unroll
         for (int m = 32; m > 0; m >>= 1) {
@@ -1178,6 +1317,15 @@ void score_topk_f32_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     score_topk_lds_body<LGX_DTYPE_F32, KSTEPS, MINMAX, MODE, kF32LdsWaves, 2, false>(
         smem, a, xcd_affine, n_utiles, nbuf);
+}
+
+// the fp32 walk's dense modes (lgx_score_dense / lgx_strat_labels_fused in fp32, d = 64 KS / 4)
+template <int KSTEPS, int MODE>
+__global__ __launch_bounds__(kF32LdsWaves * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void score_walk_f32_lds(ScoreArgs a, WalkOut o, int xcd_affine, int64_t n_utiles, int nbuf) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    score_topk_lds_body<LGX_DTYPE_F32, KSTEPS, false, MODE, kF32LdsWaves, 2, false>(smem, a, xcd_affine, n_utiles,
+                                                                                   nbuf, o);
 }
 
 __global__ void minmax_finish(const uint32_t* mm, float* out) {
@@ -1423,11 +1571,6 @@ int kch_for(int dtype, int64_t d) {
 // (col, h) ends a tile holding 16 scores of ONE user (user u0 + col, items tile_row(r, h)): the
 // labels of items 8q + 4h + 0..3 pack into one dword store.  A label is the count of thresholds the
 // score reaches (lgx_strat_thresholds); nothing but the int8 labels leaves the chip.
-struct StratThr {
-    float t[32];
-    int n;
-    float base, inv;  // estimate: floor((s - base) * inv) is the label within +-1 (thresholds ~ evenly spaced)
-};
 
 // the label estimate of the kernel, on the host (same f32 operations, no contraction)
 inline int strat_estimate(float sc, const StratThr& thr) {
@@ -1472,9 +1615,7 @@ inline bool strat_estimate_within_one(const StratThr& thr) {
     }
 }
 
-// label counts of the workgroup's 256 users kept in LDS (stride 17: the 32 users of a wave sit in
-// 32 different banks), added to the global histogram once per workgroup
-constexpr int kHistStride = 17;
+// (strat_label_lds keeps the label counts of its 256 users in LDS the same way, kHistStride)
 
 template <int DT, int KCH, bool VEC4, bool EST1>
 __global__ __launch_bounds__(kDenseWaves * 64) void strat_label_lds(const void* Q, const int64_t* user_rows,
@@ -1539,17 +1680,7 @@ __global__ __launch_bounds__(kDenseWaves * 64) void strat_label_lds(const void* 
             *reinterpret_cast<uint4*>(&img[buf][r * RB + ((q ^ (r & 15)) * 16)]) = nx[j];
         }
     };
-    auto label = [&](float sc) {
-        const float x = (sc - thr.base) * thr.inv;
-        int l = (x >= (float)thr.n || x != x) ? thr.n : (x < 0.0f ? 0 : (int)x);  // NaN -> n, as label_of
-        if (EST1) {  // the host proved |estimate - label| <= 1: one branch-free step each way
-            const float2 tp = TP[l];  // T[l], T[l + 1]
-            return (uint32_t)(l - (sc < tp.x && l > 0 ? 1 : 0) + (sc >= tp.y && l < thr.n ? 1 : 0));
-        }
-        while (l > 0 && sc < T[l]) --l;  // exact whatever the estimate
-        while (l < thr.n && sc >= T[l + 1]) ++l;
-        return (uint32_t)l;
-    };
+    auto label = [&](float sc) { return strat_label_of<EST1>(sc, thr, T, TP); };
     if (i_begin >= i_end) return;  // workgroup-uniform
     load_tile(i_begin);
     store_tile(0);
@@ -1794,6 +1925,54 @@ int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream, int d
             return LGX_ERR_UNSUPPORTED;
     }
 #undef LGX_SL
+}
+
+// The fp32 walk's dense modes (score_walk_f32_lds): d a multiple of 64 up to 256.  lgx_score_dense
+// and lgx_strat_labels_fused route fp32 through it by the same rule, so the fused labels are the
+// labels of lgx_score_dense's scores bit for bit at every d.
+inline bool f32_walk_eligible(int dtype, int64_t d) { return dtype == LGX_DTYPE_F32 && d % 64 == 0 && d >= 64 && d <= 256; }
+
+template <int KS, int MODE>
+int launch_f32_walk_ks(const ScoreArgs& a, const WalkOut& o, int xcd_affine, int64_t n_ut, hipStream_t stream) {
+    typedef LdsGeom<KS, kF32LdsWaves, 2, 4> G;
+    const size_t extra = MODE == kStratLabels ? (size_t)G::USERS * kHistStride * 4 + 34 * 8 + 34 * 4 : 0;
+    const int nbuf = lds_ring_buffers(G::TILE, extra, 1);
+    const size_t shmem = (size_t)nbuf * G::TILE + extra;
+    int rc = set_lds_limit(score_walk_f32_lds<KS, MODE>, shmem);
+    if (rc) return rc;
+    score_walk_f32_lds<KS, MODE><<<(unsigned)(n_ut * a.n_splits), kF32LdsWaves * 64, shmem, stream>>>(
+        a, o, xcd_affine, n_ut, nbuf);
+    LGX_LAUNCH_CHECK();
+    return LGX_OK;
+}
+
+// one launch over every (user tile, catalog split): splits (a multiple of 8 when more than one, so
+// the workgroups of an XCD share a split's tiles in its L2) until >= 2 rounds of the 256 resident
+// workgroups, each split >= 8 tiles; no list-filling phase to repeat, so splitting costs nothing
+template <int MODE>
+int launch_f32_walk(const void* Q, const int64_t* user_rows, const void* items, int64_t B, int64_t n_items, int64_t d,
+                    const WalkOut& o, hipStream_t stream) {
+    const int64_t n_ut = ceil_div(B, (int64_t)kF32LdsWaves * kUsersPerWave);
+    const int64_t tiles = ceil_div(n_items, (int64_t)kTileItems);
+    int64_t s = 1;
+    if (n_ut < 2 * lds_resident()) {
+        s = std::min(ceil_div((int64_t)2 * lds_resident(), n_ut), std::max<int64_t>(1, tiles / 8));
+        if (s > 8) s = 8 * (s / 8);
+    }
+    const int64_t per = ceil_div(tiles, s) * kTileItems;
+    const int n = (int)ceil_div(n_items, per);
+    LGX_REQUIRE(n_ut * n < (1LL << 31), LGX_ERR_UNSUPPORTED, "score walk: %lld users is too many", (long long)B);
+    ScoreArgs a{Q, user_rows, items, B, n_items, d, nullptr, nullptr, 1, n, per, nullptr, nullptr, nullptr, nullptr};
+    const int affine = n % 8 == 0 ? 1 : 0;
+    switch (d / 16) {
+        case 4: return launch_f32_walk_ks<4, MODE>(a, o, affine, n_ut, stream);
+        case 8: return launch_f32_walk_ks<8, MODE>(a, o, affine, n_ut, stream);
+        case 12: return launch_f32_walk_ks<12, MODE>(a, o, affine, n_ut, stream);
+        case 16: return launch_f32_walk_ks<16, MODE>(a, o, affine, n_ut, stream);
+        default:
+            set_error("score walk: no f32 walk for d=%lld", (long long)d);
+            return LGX_ERR_UNSUPPORTED;
+    }
 }
 
 // A batch runs as up to two launches over user ranges.  In the LDS kernel's full-sweep mode every
@@ -2048,6 +2227,14 @@ extern "C" int lgx_score_dense(const void* Q, const int64_t* user_rows, const vo
     LGX_REQUIRE(d > 0 && d % vec == 0 && kch > 0, LGX_ERR_UNSUPPORTED,
                 "lgx_score_dense: d=%lld must be a multiple of %lld and <= 256", (long long)d, (long long)vec);
     if (B == 0 || n_items == 0) return LGX_OK;
+    if (f32_walk_eligible(dtype, d)) {  // fp32: the 16x16x4 LDS-ring walk
+        LGX_REQUIRE(n_items < INT32_MAX, LGX_ERR_UNSUPPORTED, "lgx_score_dense: %lld items", (long long)n_items);
+        WalkOut o{};
+        o.scores = scores;
+        o.vec4 = n_items % 4 == 0 && ((uintptr_t)scores & 15) == 0;
+        return apply_sigmoid ? launch_f32_walk<kDenseSigmoid>(Q, user_rows, items, B, n_items, d, o, stream)
+                             : launch_f32_walk<kDenseScores>(Q, user_rows, items, B, n_items, d, o, stream);
+    }
     // splits: a multiple of 8 (one residue class per XCD), enough workgroups to fill the chip
     const int64_t n_ug = ceil_div(B, (int64_t)kDenseUsers);
     const int64_t tiles = ceil_div(n_items, 32);
@@ -2115,17 +2302,29 @@ extern "C" int lgx_strat_labels_fused(const void* Q, const int64_t* user_rows, c
     thr.inv = num_fold > 1 && std::isfinite(thr.t[num_fold - 1]) && thr.t[num_fold - 1] > thr.t[0]
                   ? (float)(num_fold - 1) / (thr.t[num_fold - 1] - thr.t[0]) : 1.0f / inter16;
     if (B == 0 || n_items == 0) return LGX_OK;
+    const bool vec4 = n_items % 4 == 0 && ((uintptr_t)labels & 3) == 0;
+    const bool est1 = strat_estimate_within_one(thr);
+    // counts in the scoring kernel (num_fold + 1 <= 17 bins), else a counting pass over the labels
+    const bool fuse_hist = num_fold + 1 <= kHistStride;
+    if (fuse_hist) LGX_HIP_CHECK(hipMemsetAsync(hist, 0, (size_t)B * (num_fold + 1) * sizeof(int32_t), stream));
+    if (f32_walk_eligible(dtype, d)) {  // fp32: the walk of lgx_score_dense's fp32 scores
+        WalkOut o{};
+        o.labels = labels;
+        o.hist = fuse_hist ? hist : nullptr;
+        o.thr = thr;
+        o.vec4 = vec4 ? 1 : 0;
+        o.est1 = est1 ? 1 : 0;
+        int rc = launch_f32_walk<kStratLabels>(Q, user_rows, items, B, n_items, d, o, stream);
+        if (rc) return rc;
+        if (fuse_hist) return lgx_strat_mask(labels, B, n_items, num_fold, mask_indptr, mask_indices, hist, stream_);
+        return lgx_strat_hist(labels, B, n_items, num_fold, mask_indptr, mask_indices, hist, stream_);
+    }
     const int64_t n_ug = ceil_div(B, (int64_t)kDenseUsers);
     const int64_t tiles = ceil_div(n_items, 32);
     const int64_t n_splits = std::max<int64_t>(8, std::min(8 * ceil_div(ceil_div(2048, n_ug), 8), 8 * ceil_div(tiles, 8)));
     const int64_t split_items = 32 * ceil_div(tiles, n_splits);
     const int64_t grid = n_ug * n_splits;
     LGX_REQUIRE(grid < (1LL << 31), LGX_ERR_UNSUPPORTED, "lgx_strat_labels_fused: %lld users is too many", (long long)B);
-    const bool vec4 = n_items % 4 == 0 && ((uintptr_t)labels & 3) == 0;
-    const bool est1 = strat_estimate_within_one(thr);
-    // counts in the scoring kernel (num_fold + 1 <= 17 bins), else a counting pass over the labels
-    const bool fuse_hist = num_fold + 1 <= kHistStride;
-    if (fuse_hist) LGX_HIP_CHECK(hipMemsetAsync(hist, 0, (size_t)B * (num_fold + 1) * sizeof(int32_t), stream));
 #define LGX_SL3(DTV, KC, V4)                                                                                      \
     if (est1)                                                                                                     \
         strat_label_lds<DTV, KC, V4, true><<<(unsigned)grid, kDenseWaves * 64, 0, stream>>>(                      \

@@ -423,6 +423,27 @@ def test_score_dense_lds_image(dtype, d):
     assert torch.allclose(S, ref, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("B,I,d,sig,rows", [(100, 20_011, 256, True, False), (700, 3001, 192, False, True),
+                                            (66_000, 301, 64, True, False), (4100, 12_345, 128, False, False)])
+def test_score_dense_f32_walk(B, I, d, sig, rows):
+    """fp32 getUsersRating (model.py:179-184) on the 16x16x4 LDS-ring walk (score_walk_f32_lds, d a
+    multiple of 64): split catalogs (B=100: one user tile, ~500 splits; 4100 users: 33 tiles x 16
+    XCD-affine splits), a full sweep per workgroup (66,000 users = 516 user tiles), catalogs that are
+    not a multiple of the 64-item tile or of 4 (scalar tail stores), user_rows, the sigmoid; against
+    float64 at the fp32 tolerance."""
+    g = torch.Generator(device=DEV).manual_seed(B + d)
+    n_q = B + 37 if rows else B
+    Q = torch.randn(n_q, d, device=DEV, generator=g) / np.sqrt(d)
+    items = torch.randn(I, d, device=DEV, generator=g)
+    ur = torch.randperm(n_q, device=DEV, generator=g)[:B] if rows else None
+    S = lgx.score_dense(Q, items, user_rows=ur, apply_sigmoid=sig)
+    Qs = Q[ur] if rows else Q
+    ref = Qs.double() @ items.double().T
+    if sig:
+        ref = torch.sigmoid(ref)
+    assert torch.allclose(S.double(), ref, rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("shape,ld", [((40, 40_000), 40_000), ((9, 20_001), 20_001), ((33, 5000), 7001)])
 def test_topk_rows_long_strided_rows(shape, ld):
     """4 waves per row (>= 16 K columns), 4-B loads (odd widths) and a row stride above the width"""

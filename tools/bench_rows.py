@@ -417,6 +417,144 @@ def row_f4(rows, reps):
     torch.cuda.empty_cache()
 
 
+# ----------------------------------------------------------------------------------- a7 / a8 e2e
+def _eval_dataset(cfg, tmpdir):
+    """A synthetic dataset of the config's shape in the reference's txt format: every 5th edge of a
+    user (sorted by item) is a test interaction, the rest train (users with < 2 edges: train only)."""
+    from factors_of_serendipity_recommendation_amd.dataloader import Loader
+    u, i = synth_edges(cfg, 2020, DEV)
+    u, i = u.cpu().numpy(), i.cpu().numpy()
+    order = np.lexsort((i, u))
+    u, i = u[order], i[order]
+    bounds = np.searchsorted(u, np.arange(cfg.n_users + 1))
+    pos = np.arange(len(u)) - bounds[u]
+    deg = np.diff(bounds)[u]
+    test = (pos % 5 == 4) & (deg >= 2)
+    path = os.path.join(tmpdir, f"rows_eval_{cfg.name}")
+    os.makedirs(path, exist_ok=True)
+    for name, sel in (("train.txt", ~test), ("test.txt", test)):
+        uu, ii = u[sel], i[sel]
+        b = np.searchsorted(uu, np.arange(cfg.n_users + 1))
+        with open(os.path.join(path, name), "w") as f:
+            for x in range(cfg.n_users):
+                if b[x + 1] > b[x]:
+                    f.write(str(x) + " " + " ".join(map(str, ii[b[x]:b[x + 1]])) + "\n")
+    return Loader(path=path, device=DEV, cache_adj=False)
+
+
+def row_eval(rows, reps, tmpdir, cfg_name):
+    """The reference's evaluation loops end to end on a synthetic graph of the config's shape:
+    Procedure.Test (Procedure.py:96-174; evaluator.Test: one propagation, one fused score + mask +
+    top-20 launch, host metrics) and TF batch_test.test (batch_test.py:25-84; evaluator.batch_test on
+    the propagated tables: fused score + -inf mask + top-20 + fold-out curves).  Phases timed apart
+    (device synchronised between them) to give the host metric share.  CPU legs: the reference's own
+    procedure restated with its library calls on a bounded sample -- Procedure.Test recomputes the
+    K-layer propagation for every 100-user batch (model.py:180) -- extrapolated to every test user."""
+    from factors_of_serendipity_recommendation_amd import evaluator
+    from factors_of_serendipity_recommendation_amd.model import LightGCN
+    from oracle import torch_ref
+    cfg = CONFIGS[cfg_name]
+    ds = _eval_dataset(cfg, tmpdir)
+    conf = {"latent_dim_rec": cfg.d, "lightGCN_n_layers": cfg.K, "keep_prob": 0.6, "A_split": False,
+            "pretrain": 0, "dropout": 0}
+    torch.manual_seed(0)
+    model = LightGCN(conf, ds).to(DEV).eval()
+    users = list(ds.testDict.keys())
+    n_test = len(users)
+
+    def sync_t():
+        torch.cuda.synchronize()
+        return time.perf_counter()
+
+    def test_once():
+        model._eval_cache = None  # propagate again, as a call after a training epoch does
+        return evaluator.Test(ds, model, topks=[20])
+    res = test_once()
+    walls = []
+    for _ in range(reps):
+        t0 = sync_t()
+        test_once()
+        walls.append(sync_t() - t0)
+    # the same steps one by one
+    ph = {"propagation": [], "mask_csr": [], "score_topk": [], "host_metrics": []}
+    for _ in range(reps):
+        model._eval_cache = None
+        t0 = sync_t()
+        with torch.no_grad():
+            all_users, all_items = model.computer()
+        t1 = sync_t()
+        mask = ops.lists_to_device_csr(ds.getUserPosItems(users), DEV, sort=True)
+        rows_t = torch.as_tensor(users, dtype=torch.int64, device=DEV)
+        t2 = sync_t()
+        idx, _ = ops.score_topk(all_users, all_items, 20, user_rows=rows_t, mask=mask,
+                                mask_value=-float(1 << 10), apply_sigmoid=True)
+        t3 = sync_t()
+        evaluator.test_one_batch(idx.cpu().numpy(), [ds.testDict[x] for x in users], [20])
+        t4 = sync_t()
+        for k_, a_, b_ in (("propagation", t0, t1), ("mask_csr", t1, t2), ("score_topk", t2, t3),
+                           ("host_metrics", t3, t4)):
+            ph[k_].append((b_ - a_) * 1e3)
+    ph = {k_: float(np.median(v)) for k_, v in ph.items()}
+    ms = float(np.median(walls)) * 1e3
+    # CPU: Procedure.Test's per-batch body on the host (computer() + getUsersRating + mask + topk +
+    # test_one_batch), 3 batches of 100 users, extrapolated to ceil(n_test / 100) batches
+    A = model._csr
+    N = cfg.n_users + cfg.n_items
+    G = torch_ref.coo_from_csr(A.indptr.cpu().numpy(), A.indices.cpu().numpy(), A.vals.cpu().numpy(), N)
+    E0 = torch.cat([model.embedding_user.weight, model.embedding_item.weight]).detach().float().cpu()
+    torch.set_num_threads(CPU_THREADS)
+    nb = 3
+    pos_lists = ds.getUserPosItems(users[:100 * nb])
+
+    def cpu_batches():
+        for j in range(nb):
+            out = torch_ref.propagate_cpu(G, E0, cfg.K)
+            Eu, Ei = out[:cfg.n_users], out[cfg.n_users:]
+            bu = users[100 * j:100 * (j + 1)]
+            rk, _ = torch_ref.score_topk_cpu(Eu[torch.as_tensor(bu)], Ei, 20, pos_lists[100 * j:100 * (j + 1)])
+            oracle.torch_style_metrics(rk.numpy(), [ds.testDict[x] for x in bu], [20])
+    s = cpu_s(cpu_batches)
+    n_batches = -(-n_test // 100)
+    emit(rows, f"a7 Procedure.Test end to end, {cfg.name} shape (evaluator.Test)", ms, n_test, "test users/s", "hbm",
+         0, 100 * nb, s,
+         f"{nb} of the reference's 100-user batches (K={cfg.K} torch.sparse.mm propagation + matmul + sigmoid + "
+         f"mask + torch.topk + per-user metric loops each), extrapolated to {n_batches} batches", CPU_THREADS,
+         f"{cfg.n_users} x {cfg.n_items}, {A.nnz} nnz, K={cfg.K}, d={cfg.d} fp32, {n_test} test users; phases (ms): "
+         + ", ".join(f"{k_} {v:.2f}" for k_, v in ph.items())
+         + f"; host share (mask lists + metrics) {(ph['mask_csr'] + ph['host_metrics']) / sum(ph.values()):.2f}; "
+           f"recall@20 {float(res['recall'][0]):.5f} (synthetic graph)")
+    rows[-1]["roofline"] = {"bound": "latency", "note": "end-to-end loop: phases above; kernels have their own rows"}
+    rows[-1]["phases_ms"] = ph
+    # TF batch_test on the propagated tables (LightGCN.py:148 ratings, batch_test.py:47-83)
+    with torch.no_grad():
+        all_users, all_items = model.computer()
+    train_items = {x: ds.allPos[x] for x in users}
+    test_set = {x: ds.testDict[x] for x in users}
+    evaluator.batch_test(all_users, all_items, users, train_items, test_set, Ks=[20])
+    bw = []
+    for _ in range(reps):
+        t0 = sync_t()
+        evaluator.batch_test(all_users, all_items, users, train_items, test_set, Ks=[20])
+        bw.append(sync_t() - t0)
+    ms_b = float(np.median(bw)) * 1e3
+    Eu_h, Ei_h = all_users.float().cpu(), all_items.float().cpu()
+    bu = users[:1024]
+
+    def cpu_tf_batch():  # one 1024-user batch: fp32 ratings, -inf train mask, the C++ evaluator restated
+        rate = torch.matmul(Eu_h[torch.as_tensor(bu)], Ei_h.t()).numpy()
+        for j, x in enumerate(bu):
+            rate[j][np.asarray(train_items[x], dtype=np.int64)] = -np.inf
+        oracle.eval_score_matrix_foldout(rate, [test_set[x] for x in bu], 20)
+    s_b = cpu_s(cpu_tf_batch)
+    emit(rows, f"a8 TF batch_test end to end, {cfg.name} shape (evaluator.batch_test)", ms_b, n_test, "test users/s",
+         "hbm", 0, len(bu), s_b, f"one 1024-user batch: fp32 torch.matmul ratings + -inf mask + the oracle's C "
+                                 f"restatement of the C++ top-K / fold-out evaluator (1 thread), extrapolated",
+         CPU_THREADS, f"{n_test} test users on the propagated tables (propagation not included)")
+    rows[-1]["roofline"] = {"bound": "latency", "note": "end-to-end loop over host lists and one fused launch"}
+    del model, ds, G
+    torch.cuda.empty_cache()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "rows.json"))
@@ -436,7 +574,9 @@ def main():
              ("a10", lambda r: row_a10(r, args.reps)), ("a12", lambda r: row_a12(r, args.reps)),
              ("f1", lambda r: row_f1(r, args.reps)), ("f2", lambda r: row_f2(r, args.reps)),
              ("f2b", lambda r: row_f2b(r, args.reps, tmpdir)),
-             ("f3", lambda r: row_f3(r, args.reps, tmpdir)), ("f4", lambda r: row_f4(r, args.reps))]
+             ("f3", lambda r: row_f3(r, args.reps, tmpdir)), ("f4", lambda r: row_f4(r, args.reps)),
+             ("eval_c1", lambda r: row_eval(r, args.reps, tmpdir, "gowalla")),
+             ("eval_c3", lambda r: row_eval(r, args.reps, tmpdir, "amazon"))]
     rows = []
     failed = []
     for name, fn in steps:
