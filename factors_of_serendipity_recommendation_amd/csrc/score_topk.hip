@@ -105,6 +105,14 @@ struct ScoreArgs {
     // floor_items items of each split, read by an unseeded sweep as every list's starting threshold
     float* floor;
     int64_t floor_items;
+    // candidate sweep (kCandidates): every score at or above its user's floor is appended, as a key,
+    // to cand[(b * 4 + q4) * cand_cap + n] (n = cand_cnt[b * 4 + q4]++: the 4 lanes of a user in the
+    // MFMA layout own a region each); a region that overflows flags its user tile in tile_flags.
+    // kTopK reads tile_flags as a filter: only flagged user tiles run (the exact fallback)
+    uint64_t* cand;
+    int32_t* cand_cnt;
+    int cand_cap;
+    int32_t* tile_flags;
 };
 
 // Candidates whose mask test the Bloom filter cannot settle ("suspects", ~10 % of the survivors) are
@@ -708,6 +716,12 @@ constexpr int kDenseScores = 3;
 constexpr int kDenseSigmoid = 4;
 constexpr int kStratLabels = 5;
 __host__ __device__ constexpr bool dense_mode(int m) { return m == kDenseScores || m == kDenseSigmoid || m == kStratLabels; }
+// kCandidates: the sweep without a running top-k.  Each user's threshold is its score floor (a lower
+// bound of its k-th best, kFloorOnly) and stays fixed; every score at or above it leaves the tile
+// as a packed key appended to the user's candidate regions in HBM (fire-and-forget stores, no LDS
+// lists, no drains, no Bloom filter: the mask and the exact top-k are applied per user afterwards by
+// score_topk_cand_select).  ~k * I / (group size * 0.7) candidates per user (1,450 at I = 1M).
+constexpr int kCandidates = 6;
 
 struct StratThr {
     float t[32];
@@ -730,6 +744,14 @@ __device__ __forceinline__ uint32_t strat_label_of(float sc, const StratThr& thr
     while (l > 0 && sc < T[l]) --l;
     while (l < thr.n && sc >= T[l + 1]) ++l;
     return (uint32_t)l;
+}
+
+// the reference's sigmoid (model.py:183) over dense score matrices: exp2 and reciprocal on the
+// transcendental unit, ~1e-6 relative to 1 / (1 + e^-x) (tests: 1e-5); the exact expf / IEEE division
+// form is ~20 VALU per score and made the bf16 [4096, 1M] getUsersRating VALU-bound (3.67 -> 5.37 ms).
+// Limits hold: x -> -inf gives rcp(inf) = 0, x -> +inf rcp(1) = 1.
+__device__ __forceinline__ float fast_sigmoid(float x) {
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.44269504088896341f));
 }
 
 // outputs of the dense modes
@@ -825,7 +847,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
                                                     int64_t n_utiles, int nbuf, const WalkOut& o = WalkOut{}) {
     constexpr bool F32 = DT == LGX_DTYPE_F32;
     static_assert(NACC == 2 && (F32 || KSTEPS % 2 == 0), "16x16 walk: 64-item tiles, bf16 d a multiple of 32");
-    static_assert(!dense_mode(MODE) || (F32 && !STAGGER && !MINMAX), "dense modes: the fp32 walk");
+    static_assert(!dense_mode(MODE) || (F32 && !MINMAX), "dense modes: the fp32 walk");
     // SKIP: the fast-path test runs on the MFMA output layout itself (lane l holds 16 scores of user
     // l & 15 and 16 of user 16 + (l & 15)); the regroup into the top-k layout (16 v_permlane16_swap)
     // is paid only by tiles that have a survivor.  Min / max needs every score: not with MINMAX.
@@ -882,12 +904,15 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         for (int s2 = 0; s2 < NS; ++s2)
             uf[ub * NS + s2] = __builtin_bit_cast(uint4, F::load(a.Q, qr, a.d, 2 * s2 + (q4 >> 1), q4 & 1, ok));
     }
+    if (MODE == kTopK && a.tile_flags && a.tile_flags[utile] == 0) return;  // exact fallback: flagged tiles only
     TopK st;
     st.init(lk, lk + list_keys_per_wave(k), k, lane, b, user_ok);
-    st.enable_suspects(a);
-    st.build_bloom(a);
-    if (a.seed_score) st.seed(a);
-    else if (MODE != kFloorOnly && a.floor && user_ok) st.tau = a.floor[b * a.n_splits + split];
+    if constexpr (MODE != kCandidates) {
+        st.enable_suspects(a);
+        st.build_bloom(a);
+        if (a.seed_score) st.seed(a);
+        else if (MODE != kFloorOnly && a.floor && user_ok) st.tau = a.floor[b * a.n_splits + split];
+    }
     // consume the prologue loads here: otherwise the compiler treats them as possibly pending at
     // the loop header and waits vmcnt(0) -- i.e. for the tile prefetch -- in every iteration
 #pragma unroll
@@ -947,10 +972,10 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(ahead, ntiles) - 1));
     __syncthreads();
     int buf = 0, sbuf = ahead;  // buffer of tile t / of tile t + ahead
-    // dense modes: every wave writes a tile's scores after the barrier that follows its MFMAs, so the
-    // stores are younger than the next refill and have a tile of MFMAs to drain before the next
-    // vmcnt wait (which would otherwise wait for them)
-    const bool late = (STAGGER && MODE != kMinMaxOnly && wave >= WAVES / 2) || dense_mode(MODE);  // wave-uniform
+    // staggered: the upper half of the waves runs each epilogue one tile late (below).  The unstaggered
+    // dense walk runs every epilogue late: its stores are then younger than the next refill and have
+    // a tile of MFMAs to drain before the next vmcnt wait, which would otherwise wait for them
+    const bool late = STAGGER ? MODE != kMinMaxOnly && wave >= WAVES / 2 : dense_mode(MODE);  // wave-uniform
     f32x16 acc0, acc1;  // late waves: tile t-1's scores, held across the barrier
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     f32x4 c[2][4];      // 16x16x32 accumulators: c[ub][ib] = items 16 ib + 4 (lane >> 4) + reg, user 16 ub + (lane & 15)
@@ -962,6 +987,18 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         tauB = __shfl(st.tau, 16 + (lane & 15));
     };
     if (SKIP) refresh_taus();
+    // kCandidates: this lane's two users (16 ub + r16) -- fixed thresholds, candidate counts, regions
+    const int64_t cuA = utile * G::USERS + wave * kUsersPerWave + r16, cuB = cuA + 16;
+    int cntA = 0, cntB = 0;
+    uint64_t* candA = nullptr;
+    uint64_t* candB = nullptr;
+    if constexpr (MODE == kCandidates) {
+        // padding users take +inf: never a candidate
+        tauA = cuA < a.B ? a.floor[cuA * a.n_splits + split] : INFINITY;
+        tauB = cuB < a.B ? a.floor[cuB * a.n_splits + split] : INFINITY;
+        candA = a.cand + ((size_t)(cuA < a.B ? cuA : 0) * 4 + q4) * a.cand_cap;
+        candB = a.cand + ((size_t)(cuB < a.B ? cuB : 0) * 4 + q4) * a.cand_cap;
+    }
     // regroup: swap(X = user block 0, Y = user block 1) between rows 2m and 2m+1 (lanes l, l^16)
     // leaves X' = items 16 ib + 8 h + reg, Y' = items 16 ib + 8 h + 4 + reg of user l & 31
     auto regroup = [&]() {
@@ -1093,8 +1130,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
                 const int off = 16 * ib + 4 * q4;
                 float v[4];
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    v[r] = MODE == kDenseSigmoid ? 1.0f / (1.0f + expf(-c[ub][ib][r])) : c[ub][ib][r];
+                for (int r = 0; r < 4; ++r) v[r] = MODE == kDenseSigmoid ? fast_sigmoid(c[ub][ib][r]) : c[ub][ib][r];
                 if (o.vec4 && off + 4 <= rem) {
                     *reinterpret_cast<float4*>(row + off) = make_float4(v[0], v[1], v[2], v[3]);
                 } else {
@@ -1136,7 +1172,46 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
             }
         }
     };
+    // kCandidates: lane (q4, r16) holds items e0 + 16 ib + 4 q4 + reg of users cuA (c[0]) and cuB (c[1])
+    auto cand_tile = [&](int64_t e0) {
+        const bool tail = e0 + G::TILE_ITEMS > i_end;
+        float m0 = c[0][0][0], m1 = c[1][0][0];
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                m0 = fmaxf(m0, c[0][ib][r]);
+                m1 = fmaxf(m1, c[1][ib][r]);
+            }
+        if (__ballot((m0 >= tauA) | (m1 >= tauB)) == 0ull) return;  // wave-uniform fast path
+        const int32_t rem = tail ? (int32_t)(i_end - e0) : G::TILE_ITEMS;
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib) {
+            const float a0 = fmaxf(fmaxf(c[0][ib][0], c[0][ib][1]), fmaxf(c[0][ib][2], c[0][ib][3]));
+            const float a1 = fmaxf(fmaxf(c[1][ib][0], c[1][ib][1]), fmaxf(c[1][ib][2], c[1][ib][3]));
+            if (__ballot((a0 >= tauA) | (a1 >= tauB)) == 0ull) continue;  // no candidate in this item block
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int off = 16 * ib + 4 * q4 + r;
+                const int32_t item = (int32_t)(e0 + off);
+                const bool in = off < rem;
+                const float s0 = c[0][ib][r], s1 = c[1][ib][r];
+                if (in && s0 >= tauA) {
+                    if (cntA < a.cand_cap) candA[cntA] = make_key(s0, item);
+                    ++cntA;
+                }
+                if (in && s1 >= tauB) {
+                    if (cntB < a.cand_cap) candB[cntB] = make_key(s1, item);
+                    ++cntB;
+                }
+            }
+        }
+    };
     auto epilogue = [&](int64_t e0) {
+        if constexpr (MODE == kCandidates) {
+            cand_tile(e0);
+            return;
+        }
         if constexpr (MODE == kDenseScores || MODE == kDenseSigmoid) {
             dense_tile(e0);
             return;
@@ -1238,6 +1313,12 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         return;
     }
     if constexpr (MODE == kDenseScores || MODE == kDenseSigmoid) return;
+    if constexpr (MODE == kCandidates) {
+        if (cuA < a.B) a.cand_cnt[cuA * 4 + q4] = cntA;
+        if (cuB < a.B) a.cand_cnt[cuB * 4 + q4] = cntB;
+        if (__ballot(cntA > a.cand_cap || cntB > a.cand_cap) != 0ull && lane == 0) a.tile_flags[utile] = 1;
+        return;
+    }
     if constexpr (MODE == kMinMaxOnly) {
 #pragma unroll
         for (int m = 32; m > 0; m >>= 1) {
@@ -1319,13 +1400,21 @@ void score_topk_f32_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf)
         smem, a, xcd_affine, n_utiles, nbuf);
 }
 
-// the fp32 walk's dense modes (lgx_score_dense / lgx_strat_labels_fused in fp32, d = 64 KS / 4)
+// the fp32 walk's dense modes (lgx_score_dense / lgx_strat_labels_fused in fp32, d = 4 KS).  d <= 128:
+// 8 waves x 32 users, two per SIMD, staggered as the bf16 top-k walk is -- one wave's epilogue (labels
+// and their counts, or the score stores) runs beside its partner's MFMAs.  With one wave per SIMD (the
+// f32 top-k shape) the d=64 labels took 10.6 ms per 4096 x 1M batch: nothing issued MFMAs during an
+// epilogue.  d >= 192: the 32 users' rows take 96-128 VGPRs, two waves per SIMD spill (d=256: 72 B of
+// scratch), and a tile is 12-16 K MFMA cycles per wave against a ~1 K-cycle epilogue: 4 waves, one per
+// SIMD, every epilogue after the barrier.
+__host__ __device__ constexpr int walk_waves(int ks) { return ks <= 8 ? 8 : 4; }
 template <int KSTEPS, int MODE>
-__global__ __launch_bounds__(kF32LdsWaves * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+__global__ __launch_bounds__(walk_waves(KSTEPS) * 64)
+__attribute__((amdgpu_waves_per_eu(walk_waves(KSTEPS) / 4, walk_waves(KSTEPS) / 4)))
 void score_walk_f32_lds(ScoreArgs a, WalkOut o, int xcd_affine, int64_t n_utiles, int nbuf) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    score_topk_lds_body<LGX_DTYPE_F32, KSTEPS, false, MODE, kF32LdsWaves, 2, false>(smem, a, xcd_affine, n_utiles,
-                                                                                   nbuf, o);
+    score_topk_lds_body<LGX_DTYPE_F32, KSTEPS, false, MODE, walk_waves(KSTEPS), 2, walk_waves(KSTEPS) == 8>(
+        smem, a, xcd_affine, n_utiles, nbuf, o);
 }
 
 __global__ void minmax_finish(const uint32_t* mm, float* out) {
@@ -1334,23 +1423,14 @@ __global__ void minmax_finish(const uint32_t* mm, float* out) {
 }
 
 // one wave per query: merge the split lists, masked tail, optional sigmoid (k <= 64 R)
+// the merged list of user b -> out_idx / out_val (k <= 64 R): keys in order, then -- when fewer than k
+// unmasked items exist -- the user's masked items with mask_value (Procedure.py:134 ranks them below
+// every real score); the optional sigmoid on the scores (model.py:183)
 template <int R>
-__global__ __launch_bounds__(64) void score_topk_finalize(ScoreArgs a, float mask_value, int apply_sigmoid,
-                                                          int32_t* __restrict__ out_idx, float* __restrict__ out_val,
-                                                          float* __restrict__ minmax_out) {
-    const int lane = threadIdx.x;
-    const int64_t b = blockIdx.x;
+__device__ __forceinline__ void emit_topk(const WaveList<R>& top, const ScoreArgs& a, int64_t b, int lane,
+                                          float mask_value, int apply_sigmoid, int32_t* __restrict__ out_idx,
+                                          float* __restrict__ out_val) {
     const int k = a.k;
-    const int64_t total = (int64_t)a.n_splits * k;
-    const float* ps = a.part_score + (size_t)b * total;
-    const int32_t* pi = a.part_idx + (size_t)b * total;
-    WaveList<R> top;
-    top.clear();
-    for (int64_t base = 0; base < total; base += 64) {
-        const int64_t j = base + lane;
-        const uint64_t cand = (j < total && pi[j] >= 0) ? make_key(ps[j], pi[j]) : 0ull;
-        top.push(cand, k, lane);
-    }
     int n_real = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) n_real += __popcll(__ballot(top.t[r] != 0ull));
@@ -1373,10 +1453,69 @@ __global__ __launch_bounds__(64) void score_topk_finalize(ScoreArgs a, float mas
         out_idx[b * k + e] = idx;
         if (out_val) out_val[b * k + e] = val;
     }
+}
+
+// user b's split lists (the LDS walk's flush) merged into one top-k
+template <int R>
+__device__ __forceinline__ void merge_parts(WaveList<R>& top, const ScoreArgs& a, int64_t b, int lane) {
+    const int k = a.k;
+    const int64_t total = (int64_t)a.n_splits * k;
+    const float* ps = a.part_score + (size_t)b * total;
+    const int32_t* pi = a.part_idx + (size_t)b * total;
+    for (int64_t base = 0; base < total; base += 64) {
+        const int64_t j = base + lane;
+        const uint64_t cand = (j < total && pi[j] >= 0) ? make_key(ps[j], pi[j]) : 0ull;
+        top.push(cand, k, lane);
+    }
+}
+
+// one wave per query: merge the split lists, masked tail, optional sigmoid (k <= 64 R)
+template <int R>
+__global__ __launch_bounds__(64) void score_topk_finalize(ScoreArgs a, float mask_value, int apply_sigmoid,
+                                                          int32_t* __restrict__ out_idx, float* __restrict__ out_val,
+                                                          float* __restrict__ minmax_out) {
+    const int lane = threadIdx.x;
+    const int64_t b = blockIdx.x;
+    WaveList<R> top;
+    top.clear();
+    merge_parts(top, a, b, lane);
+    emit_topk(top, a, b, lane, mask_value, apply_sigmoid, out_idx, out_val);
     if (minmax_out && b == 0 && lane == 0) {
         minmax_out[0] = unord_f32(a.minmax[0]);
         minmax_out[1] = unord_f32(a.minmax[1]);
     }
+}
+
+// kCandidates' second half, one wave per query: the exact top-k of the user's candidate keys (every
+// score at or above its floor), masked items dropped -- tested only for keys above the running k-th
+// best, ~k ln(n / k) of them -- in the same key order (score, then the lower index) as the running
+// walk, so the lists are the walk's lists.  A user whose tile overflowed a candidate region takes the
+// exact fallback's split lists instead.
+template <int R>
+__global__ __launch_bounds__(64) void score_topk_cand_select(ScoreArgs a, int64_t tile_users, float mask_value,
+                                                             int apply_sigmoid, int32_t* __restrict__ out_idx,
+                                                             float* __restrict__ out_val) {
+    const int lane = threadIdx.x;
+    const int64_t b = blockIdx.x;
+    const int k = a.k;
+    WaveList<R> top;
+    top.clear();
+    if (a.tile_flags[b / tile_users]) {
+        merge_parts(top, a, b, lane);
+    } else {
+        for (int q = 0; q < 4; ++q) {
+            const int n = min(a.cand_cnt[b * 4 + q], a.cand_cap);
+            const uint64_t* src = a.cand + ((size_t)b * 4 + q) * a.cand_cap;
+            for (int base = 0; base < n; base += 64) {
+                const int j = base + lane;
+                uint64_t key = j < n ? src[j] : 0ull;
+                const uint64_t thr = top.at(k - 1);  // all lanes (a shuffle)
+                if (a.mask_indptr && key > thr && is_masked(a, b, key_index(key))) key = 0ull;
+                top.push(key, k, lane);
+            }
+        }
+    }
+    emit_topk(top, a, b, lane, mask_value, apply_sigmoid, out_idx, out_val);
 }
 
 __global__ void minmax_init(uint32_t* mm) {
@@ -1441,7 +1580,7 @@ __global__ __launch_bounds__(kDenseWaves * 64) void score_dense_kernel(const voi
             const int64_t u = u0 + tile_row(r, h);
             if (u < B) {
                 const float sc = acc[r];
-                out[u * n_items + item_row] = SIG ? 1.0f / (1.0f + expf(-sc)) : sc;
+                out[u * n_items + item_row] = SIG ? fast_sigmoid(sc) : sc;
             }
         }
     }
@@ -1543,7 +1682,7 @@ void score_dense_lds(const void* Q, const int64_t* user_rows, const void* items,
                     if (u0 + tile_row(r, h) < B) {
                         const float sc = acc[r];
                         char* base = reinterpret_cast<char*>(out + (u0 + tile_row(r, 0)) * n_items + i0);
-                        *reinterpret_cast<float*>(base + boff) = SIG ? 1.0f / (1.0f + expf(-sc)) : sc;
+                        *reinterpret_cast<float*>(base + boff) = SIG ? fast_sigmoid(sc) : sc;
                     }
                 }
             }
@@ -1857,7 +1996,8 @@ inline int lds_ring_buffers(size_t tile, size_t lists, int wg_per_cu) {
 template <int KS, bool MM, int MODE>
 int launch_bf16_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     typedef LdsGeom<KS, kBf16LdsWaves, 2> G;
-    const size_t lists = (size_t)kBf16LdsWaves * list_bytes_per_wave(a.k, kPendBf16Lds);
+    // the candidate sweep keeps no lists in LDS: the ring takes it (4 tiles at d = 256)
+    const size_t lists = MODE == kCandidates ? 0 : (size_t)kBf16LdsWaves * list_bytes_per_wave(a.k, kPendBf16Lds);
     const int nbuf = lds_ring_buffers(G::TILE, lists, 1);
     const size_t shmem = (size_t)nbuf * G::TILE + lists;
     int rc = set_lds_limit(score_topk_bf16_lds<KS, MM, MODE>, shmem);
@@ -1891,13 +2031,13 @@ int launch_f32_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t st
 template <bool MM, int MODE = kTopK>
 int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream, int dtype = LGX_DTYPE_BF16) {
     const int ksteps = (int)(a.d / 16);
-    if constexpr (MODE == kFloorOnly) {
+    if constexpr (MODE == kFloorOnly || MODE == kCandidates) {
         if (dtype == LGX_DTYPE_F32) {
-            set_error("lgx_score_topk: score floors are a bf16 LDS kernel mode");
+            set_error("lgx_score_topk: score floors and candidate sweeps are bf16 LDS kernel modes");
             return LGX_ERR_UNSUPPORTED;
         }
     }
-    if constexpr (MODE != kFloorOnly) {
+    if constexpr (MODE != kFloorOnly && MODE != kCandidates) {
         if (dtype == LGX_DTYPE_F32) {
             switch (ksteps) {
                 case 4: return launch_f32_lds_kernel<4, MM, MODE>(a, p, stream);
@@ -1934,13 +2074,13 @@ inline bool f32_walk_eligible(int dtype, int64_t d) { return dtype == LGX_DTYPE_
 
 template <int KS, int MODE>
 int launch_f32_walk_ks(const ScoreArgs& a, const WalkOut& o, int xcd_affine, int64_t n_ut, hipStream_t stream) {
-    typedef LdsGeom<KS, kF32LdsWaves, 2, 4> G;
+    typedef LdsGeom<KS, walk_waves(KS), 2, 4> G;
     const size_t extra = MODE == kStratLabels ? (size_t)G::USERS * kHistStride * 4 + 34 * 8 + 34 * 4 : 0;
     const int nbuf = lds_ring_buffers(G::TILE, extra, 1);
     const size_t shmem = (size_t)nbuf * G::TILE + extra;
     int rc = set_lds_limit(score_walk_f32_lds<KS, MODE>, shmem);
     if (rc) return rc;
-    score_walk_f32_lds<KS, MODE><<<(unsigned)(n_ut * a.n_splits), kF32LdsWaves * 64, shmem, stream>>>(
+    score_walk_f32_lds<KS, MODE><<<(unsigned)(n_ut * a.n_splits), walk_waves(KS) * 64, shmem, stream>>>(
         a, o, xcd_affine, n_ut, nbuf);
     LGX_LAUNCH_CHECK();
     return LGX_OK;
@@ -1952,7 +2092,7 @@ int launch_f32_walk_ks(const ScoreArgs& a, const WalkOut& o, int xcd_affine, int
 template <int MODE>
 int launch_f32_walk(const void* Q, const int64_t* user_rows, const void* items, int64_t B, int64_t n_items, int64_t d,
                     const WalkOut& o, hipStream_t stream) {
-    const int64_t n_ut = ceil_div(B, (int64_t)kF32LdsWaves * kUsersPerWave);
+    const int64_t n_ut = ceil_div(B, (int64_t)walk_waves((int)(d / 16)) * kUsersPerWave);
     const int64_t tiles = ceil_div(n_items, (int64_t)kTileItems);
     int64_t s = 1;
     if (n_ut < 2 * lds_resident()) {
@@ -1991,8 +2131,21 @@ size_t range_susp_bytes(const UserRange& r) {
 }
 // the LDS kernel's score floors [users, n_splits]
 size_t range_floor_bytes(const UserRange& r) { return r.p.lds ? align_up((size_t)(r.u1 - r.u0) * r.p.n_splits * 4) : 0; }
-size_t range_ws_bytes(const UserRange& r, int k) {
-    return 2 * range_list_bytes(r, k) + range_susp_bytes(r) + range_floor_bytes(r);
+// the candidate sweep (kCandidates + score_topk_cand_select): bf16 full sweeps of >= 256 K items.
+// Candidate regions of kCandCap keys per user and lane: floors over 16 384 items leave ~1,450
+// candidates per user at 1 M items, ~360 per region, sd ~19; a region past its cap flags the user
+// tile for the exact fallback (the running walk over that tile).
+constexpr int kCandCap = 512;
+inline bool cand_sweep(const SplitPlan& p, bool minmax, int dtype, int64_t n_items) {
+    return p.lds && p.n_splits == 1 && !minmax && dtype == LGX_DTYPE_BF16 && n_items >= 16 * 16384;
+}
+size_t range_cand_bytes(const UserRange& r, int dtype, int64_t n_items) {
+    if (!cand_sweep(r.p, false, dtype, n_items)) return 0;
+    const int64_t n = r.u1 - r.u0;
+    return align_up((size_t)n * 4 * kCandCap * 8) + align_up((size_t)n * 4 * 4) + align_up((size_t)r.p.n_utiles * 4);
+}
+size_t range_ws_bytes(const UserRange& r, int k, int dtype, int64_t n_items) {
+    return 2 * range_list_bytes(r, k) + range_susp_bytes(r) + range_floor_bytes(r) + range_cand_bytes(r, dtype, n_items);
 }
 
 int plan_ranges(int64_t B, int64_t n_items, int dtype, int64_t d, int k, UserRange* r) {
@@ -2010,7 +2163,7 @@ int plan_ranges(int64_t B, int64_t n_items, int dtype, int64_t d, int k, UserRan
     if (full < B) r[n++] = {full, B, plan_splits(B - full, n_items, dtype, d, k), 0};
     for (int i = 0; i < n; ++i) {
         r[i].ws_off = off;
-        off += range_ws_bytes(r[i], k);
+        off += range_ws_bytes(r[i], k, dtype, n_items);
     }
     return n;
 }
@@ -2024,8 +2177,8 @@ int plan_ranges(int64_t B, int64_t n_items, int dtype, int64_t d, int k, UserRan
 // sweep 463.7 ms, these 7 stages 431.9 ms (-6.9 %); 2 stages -2 %, 3 stages -4 %
 // (profiles/r02_score_lab_seeded.txt, profiles/r02_score_lab_stages.txt).
 constexpr int64_t kSeedItems = 16384;
-inline bool seeded_sweep(const SplitPlan& p, bool minmax, int64_t n_items) {
-    return p.lds && p.n_splits == 1 && !minmax && n_items >= 16 * kSeedItems;
+inline bool seeded_sweep(const SplitPlan& p, bool minmax, int64_t n_items, int dtype) {
+    return p.lds && p.n_splits == 1 && !minmax && n_items >= 16 * kSeedItems && !cand_sweep(p, minmax, dtype, n_items);
 }
 // Score floors (kFloorOnly): an unseeded LDS sweep -- the first stage of a seeded sweep, or every
 // split of a split launch -- starts its lists at a floor taken from its first kFloorItems items
@@ -2046,7 +2199,7 @@ size_t topk_ws_bytes(int64_t B, int64_t n_items, int k, int dtype, int64_t d) {
     UserRange r[2];
     const int n = plan_ranges(B, n_items, dtype, d, k, r);
     size_t bytes = 0;
-    for (int i = 0; i < n; ++i) bytes += range_ws_bytes(r[i], k);
+    for (int i = 0; i < n; ++i) bytes += range_ws_bytes(r[i], k, dtype, n_items);
     return bytes + 512;  // + the global min / max words
 }
 
@@ -2080,9 +2233,10 @@ extern "C" int lgx_score_topk_plan(int64_t B, int64_t n_items, int64_t d, int dt
                                  : (v1_waves(k) == 4 ? "score_topk_kernel<4 waves>" : "score_topk_kernel<1 wave>");
         const char* mode = p.lds ? (p.n_splits == 1 ? "full-sweep" : (p.xcd_affine ? "split-xcd" : "split"))
                                  : "split";
+        const char* how = seeded_sweep(p, false, n_items, dtype) ? " (seeded in stages)"
+                          : cand_sweep(p, false, dtype, n_items) ? " (candidates above score floors)" : "";
         off += snprintf(buf + off, len - off, "%s%s users[%lld,%lld) %s%s n_splits=%d utiles=%lld",
-                        i ? "; " : "", kern, (long long)r[i].u0, (long long)r[i].u1, mode,
-                        seeded_sweep(p, false, n_items) ? " (seeded in stages)" : "", p.n_splits,
+                        i ? "; " : "", kern, (long long)r[i].u0, (long long)r[i].u1, mode, how, p.n_splits,
                         (long long)p.n_utiles);
     }
     return LGX_OK;
@@ -2134,7 +2288,33 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
             rc = launch_lds<false, kFloorOnly>(a, p, stream, dtype);
             if (rc) return rc;
         }
-        if (seeded_sweep(p, mm, n_items)) {
+        if (cand_sweep(p, mm, dtype, n_items)) {
+            // floors (above) -> every score at or above its floor into the candidate regions -> the exact
+            // fallback over the user tiles whose regions overflowed -> the per-user exact top-k
+            char* cb = wsr + 2 * list_bytes + range_susp_bytes(R) + range_floor_bytes(R);
+            ScoreArgs ca = a;
+            ca.cand = reinterpret_cast<uint64_t*>(cb);
+            ca.cand_cnt = reinterpret_cast<int32_t*>(cb + align_up((size_t)Bi * 4 * kCandCap * 8));
+            ca.cand_cap = kCandCap;
+            ca.tile_flags = reinterpret_cast<int32_t*>(cb + align_up((size_t)Bi * 4 * kCandCap * 8) +
+                                                       align_up((size_t)Bi * 4 * 4));
+            LGX_HIP_CHECK(hipMemsetAsync(ca.tile_flags, 0, (size_t)p.n_utiles * 4, stream));
+            rc = launch_lds<false, kCandidates>(ca, p, stream, dtype);
+            if (rc) return rc;
+            ScoreArgs fb = a;  // the exact fallback: the running walk, unseeded, no floor, flagged tiles only
+            fb.floor = nullptr;
+            fb.tile_flags = ca.tile_flags;
+            rc = launch_lds<false>(fb, p, stream, dtype);
+            if (rc) return rc;
+            int32_t* oi = out_idx + R.u0 * k;
+            float* ov = out_val ? out_val + R.u0 * k : nullptr;
+            const int64_t tu = (int64_t)p.waves * kUsersPerWave;
+            if (k <= 64) score_topk_cand_select<1><<<(unsigned)Bi, 64, 0, stream>>>(ca, tu, mask_value, apply_sigmoid, oi, ov);
+            else if (k <= 128) score_topk_cand_select<2><<<(unsigned)Bi, 64, 0, stream>>>(ca, tu, mask_value, apply_sigmoid, oi, ov);
+            else score_topk_cand_select<4><<<(unsigned)Bi, 64, 0, stream>>>(ca, tu, mask_value, apply_sigmoid, oi, ov);
+            LGX_LAUNCH_CHECK();
+            continue;
+        } else if (seeded_sweep(p, mm, n_items, dtype)) {
             rc = LGX_OK;
             for (int64_t lo = 0, hi = kSeedItems; lo < n_items && rc == LGX_OK; lo = hi, hi *= 2) {
                 ScoreArgs st = a;
