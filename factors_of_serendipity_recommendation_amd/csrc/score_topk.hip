@@ -105,14 +105,12 @@ struct ScoreArgs {
     // floor_items items of each split, read by an unseeded sweep as every list's starting threshold
     float* floor;
     int64_t floor_items;
-    // candidate sweep (kCandidates): every score at or above its user's floor is appended, as a key,
-    // to cand[(b * 4 + q4) * cand_cap + n] (n = cand_cnt[b * 4 + q4]++: the 4 lanes of a user in the
-    // MFMA layout own a region each); a region that overflows flags its user tile in tile_flags.
-    // kTopK reads tile_flags as a filter: only flagged user tiles run (the exact fallback)
+    // candidate sweep (kCandidates): every key at or above its lane's threshold is appended to
+    // cand[(b * 4 + q4) * cand_cap + n] (the 4 lanes of user b in the MFMA layout own a region each;
+    // cand_cnt[b * 4 + q4] = the final n)
     uint64_t* cand;
     int32_t* cand_cnt;
     int cand_cap;
-    int32_t* tile_flags;
 };
 
 // Candidates whose mask test the Bloom filter cannot settle ("suspects", ~10 % of the survivors) are
@@ -716,11 +714,14 @@ constexpr int kDenseScores = 3;
 constexpr int kDenseSigmoid = 4;
 constexpr int kStratLabels = 5;
 __host__ __device__ constexpr bool dense_mode(int m) { return m == kDenseScores || m == kDenseSigmoid || m == kStratLabels; }
-// kCandidates: the sweep without a running top-k.  Each user's threshold is its score floor (a lower
-// bound of its k-th best, kFloorOnly) and stays fixed; every score at or above it leaves the tile
-// as a packed key appended to the user's candidate regions in HBM (fire-and-forget stores, no LDS
-// lists, no drains, no Bloom filter: the mask and the exact top-k are applied per user afterwards by
-// score_topk_cand_select).  ~k * I / (group size * 0.7) candidates per user (1,450 at I = 1M).
+// kCandidates: the sweep without a running top-k in LDS.  Each lane of a user (4 per user in the MFMA
+// layout, each seeing a quarter of the items) appends every key at or above its threshold to its own
+// region in HBM (fire-and-forget stores; no LDS lists, no drains, no Bloom filter: the mask and the
+// exact top-k are applied per user afterwards by score_topk_cand_select).  The threshold starts at
+// the user's score floor (a lower bound of its k-th best, kFloorOnly): ~1,450 candidates per user at
+// I = 1M, ~360 per region.  A region about to run full is compacted in place to its own k best keys
+// and its threshold raised to the k-th of them -- valid because a key of the user's top-k is in the
+// top-k of its own region -- so no region ever overflows, whatever the data (ties included).
 constexpr int kCandidates = 6;
 
 struct StratThr {
@@ -904,7 +905,6 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         for (int s2 = 0; s2 < NS; ++s2)
             uf[ub * NS + s2] = __builtin_bit_cast(uint4, F::load(a.Q, qr, a.d, 2 * s2 + (q4 >> 1), q4 & 1, ok));
     }
-    if (MODE == kTopK && a.tile_flags && a.tile_flags[utile] == 0) return;  // exact fallback: flagged tiles only
     TopK st;
     st.init(lk, lk + list_keys_per_wave(k), k, lane, b, user_ok);
     if constexpr (MODE != kCandidates) {
@@ -987,15 +987,19 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         tauB = __shfl(st.tau, 16 + (lane & 15));
     };
     if (SKIP) refresh_taus();
-    // kCandidates: this lane's two users (16 ub + r16) -- fixed thresholds, candidate counts, regions
+    // kCandidates: this lane's two users (16 ub + r16) -- key thresholds (tauA / tauB: their scores,
+    // for the fast path), candidate counts, regions
     const int64_t cuA = utile * G::USERS + wave * kUsersPerWave + r16, cuB = cuA + 16;
     int cntA = 0, cntB = 0;
+    uint64_t thrA = ~0ull, thrB = ~0ull;  // padding users: nothing passes
     uint64_t* candA = nullptr;
     uint64_t* candB = nullptr;
     if constexpr (MODE == kCandidates) {
-        // padding users take +inf: never a candidate
-        tauA = cuA < a.B ? a.floor[cuA * a.n_splits + split] : INFINITY;
-        tauB = cuB < a.B ? a.floor[cuB * a.n_splits + split] : INFINITY;
+        // the floor key of the lowest rank: every score >= the floor passes, ties included
+        if (cuA < a.B) thrA = make_key(a.floor[cuA * a.n_splits + split], 0x7fffffff);
+        if (cuB < a.B) thrB = make_key(a.floor[cuB * a.n_splits + split], 0x7fffffff);
+        tauA = key_score(thrA);
+        tauB = key_score(thrB);
         candA = a.cand + ((size_t)(cuA < a.B ? cuA : 0) * 4 + q4) * a.cand_cap;
         candB = a.cand + ((size_t)(cuB < a.B ? cuB : 0) * 4 + q4) * a.cand_cap;
     }
@@ -1172,7 +1176,33 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
             }
         }
     };
-    // kCandidates: lane (q4, r16) holds items e0 + 16 ib + 4 q4 + reg of users cuA (c[0]) and cuB (c[1])
+    // kCandidates, lane-local and rare: the region's k best keys to its front (partial selection sort
+    // over its n keys, read back at device scope after this lane's stores have completed); returns
+    // the k-th best key, the region's new threshold
+    auto compact = [&](uint64_t* reg, int n) -> uint64_t {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (int j = 0; j < k; ++j) {
+            uint64_t m = 0;
+            int at = j;
+            for (int i = j; i < n; ++i) {
+                const uint64_t x = __hip_atomic_load(reg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (x > m) {
+                    m = x;
+                    at = i;
+                }
+            }
+            if (at != j) {
+                const uint64_t y = __hip_atomic_load(reg + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(reg + at, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(reg + j, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (j + 1 == k) return m;
+        }
+        return 0ull;
+    };
+    // kCandidates: lane (q4, r16) holds items e0 + 16 ib + 4 q4 + reg of users cuA (c[0]) and cuB (c[1]);
+    // a tile appends at most 16 keys per region, so a region is compacted once it holds more than
+    // cap - 16
     auto cand_tile = [&](int64_t e0) {
         const bool tail = e0 + G::TILE_ITEMS > i_end;
         float m0 = c[0][0][0], m1 = c[1][0][0];
@@ -1195,15 +1225,22 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
                 const int off = 16 * ib + 4 * q4 + r;
                 const int32_t item = (int32_t)(e0 + off);
                 const bool in = off < rem;
-                const float s0 = c[0][ib][r], s1 = c[1][ib][r];
-                if (in && s0 >= tauA) {
-                    if (cntA < a.cand_cap) candA[cntA] = make_key(s0, item);
-                    ++cntA;
-                }
-                if (in && s1 >= tauB) {
-                    if (cntB < a.cand_cap) candB[cntB] = make_key(s1, item);
-                    ++cntB;
-                }
+                const uint64_t k0 = make_key(c[0][ib][r], item), k1 = make_key(c[1][ib][r], item);
+                if (in && k0 >= thrA) candA[cntA++] = k0;
+                if (in && k1 >= thrB) candB[cntB++] = k1;
+            }
+        }
+        const int lim = a.cand_cap - 16;
+        if (__ballot(cntA > lim || cntB > lim) != 0ull) {  // rare: some region is nearly full
+            if (cntA > lim) {
+                thrA = compact(candA, cntA);
+                cntA = k;
+                tauA = key_score(thrA);
+            }
+            if (cntB > lim) {
+                thrB = compact(candB, cntB);
+                cntB = k;
+                tauB = key_score(thrB);
             }
         }
     };
@@ -1316,7 +1353,6 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     if constexpr (MODE == kCandidates) {
         if (cuA < a.B) a.cand_cnt[cuA * 4 + q4] = cntA;
         if (cuB < a.B) a.cand_cnt[cuB * 4 + q4] = cntB;
-        if (__ballot(cntA > a.cand_cap || cntB > a.cand_cap) != 0ull && lane == 0) a.tile_flags[utile] = 1;
         return;
     }
     if constexpr (MODE == kMinMaxOnly) {
@@ -1486,23 +1522,19 @@ __global__ __launch_bounds__(64) void score_topk_finalize(ScoreArgs a, float mas
     }
 }
 
-// kCandidates' second half, one wave per query: the exact top-k of the user's candidate keys (every
-// score at or above its floor), masked items dropped -- tested only for keys above the running k-th
-// best, ~k ln(n / k) of them -- in the same key order (score, then the lower index) as the running
-// walk, so the lists are the walk's lists.  A user whose tile overflowed a candidate region takes the
-// exact fallback's split lists instead.
+// kCandidates' second half, one wave per query: the exact top-k of the user's candidate keys, masked
+// items dropped -- tested only for keys above the running k-th best, ~k ln(n / k) of them -- in the
+// same key order (score, then the lower index) as the running walk, so the lists are its lists.
 template <int R>
-__global__ __launch_bounds__(64) void score_topk_cand_select(ScoreArgs a, int64_t tile_users, float mask_value,
-                                                             int apply_sigmoid, int32_t* __restrict__ out_idx,
+__global__ __launch_bounds__(64) void score_topk_cand_select(ScoreArgs a, float mask_value, int apply_sigmoid,
+                                                             int32_t* __restrict__ out_idx,
                                                              float* __restrict__ out_val) {
     const int lane = threadIdx.x;
     const int64_t b = blockIdx.x;
     const int k = a.k;
     WaveList<R> top;
     top.clear();
-    if (a.tile_flags[b / tile_users]) {
-        merge_parts(top, a, b, lane);
-    } else {
+    {
         for (int q = 0; q < 4; ++q) {
             const int n = min(a.cand_cnt[b * 4 + q], a.cand_cap);
             const uint64_t* src = a.cand + ((size_t)b * 4 + q) * a.cand_cap;
@@ -2132,9 +2164,9 @@ size_t range_susp_bytes(const UserRange& r) {
 // the LDS kernel's score floors [users, n_splits]
 size_t range_floor_bytes(const UserRange& r) { return r.p.lds ? align_up((size_t)(r.u1 - r.u0) * r.p.n_splits * 4) : 0; }
 // the candidate sweep (kCandidates + score_topk_cand_select): bf16 full sweeps of >= 256 K items.
-// Candidate regions of kCandCap keys per user and lane: floors over 16 384 items leave ~1,450
-// candidates per user at 1 M items, ~360 per region, sd ~19; a region past its cap flags the user
-// tile for the exact fallback (the running walk over that tile).
+// Candidate regions of kCandCap keys per user and lane (16 KB per user): floors over 16 384 items
+// leave ~1,450 candidates per user at 1 M items, ~360 per region; the floor's own spread puts a few
+// percent of the regions past the cap, which then compact in place (kCandidates).
 constexpr int kCandCap = 512;
 inline bool cand_sweep(const SplitPlan& p, bool minmax, int dtype, int64_t n_items) {
     return p.lds && p.n_splits == 1 && !minmax && dtype == LGX_DTYPE_BF16 && n_items >= 16 * 16384;
@@ -2142,7 +2174,7 @@ inline bool cand_sweep(const SplitPlan& p, bool minmax, int dtype, int64_t n_ite
 size_t range_cand_bytes(const UserRange& r, int dtype, int64_t n_items) {
     if (!cand_sweep(r.p, false, dtype, n_items)) return 0;
     const int64_t n = r.u1 - r.u0;
-    return align_up((size_t)n * 4 * kCandCap * 8) + align_up((size_t)n * 4 * 4) + align_up((size_t)r.p.n_utiles * 4);
+    return align_up((size_t)n * 4 * kCandCap * 8) + align_up((size_t)n * 4 * 4);
 }
 size_t range_ws_bytes(const UserRange& r, int k, int dtype, int64_t n_items) {
     return 2 * range_list_bytes(r, k) + range_susp_bytes(r) + range_floor_bytes(r) + range_cand_bytes(r, dtype, n_items);
@@ -2289,29 +2321,20 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
             if (rc) return rc;
         }
         if (cand_sweep(p, mm, dtype, n_items)) {
-            // floors (above) -> every score at or above its floor into the candidate regions -> the exact
-            // fallback over the user tiles whose regions overflowed -> the per-user exact top-k
+            // floors (above) -> every key at or above its lane's threshold into the candidate regions ->
+            // the per-user exact top-k of the unmasked candidates
             char* cb = wsr + 2 * list_bytes + range_susp_bytes(R) + range_floor_bytes(R);
             ScoreArgs ca = a;
             ca.cand = reinterpret_cast<uint64_t*>(cb);
             ca.cand_cnt = reinterpret_cast<int32_t*>(cb + align_up((size_t)Bi * 4 * kCandCap * 8));
             ca.cand_cap = kCandCap;
-            ca.tile_flags = reinterpret_cast<int32_t*>(cb + align_up((size_t)Bi * 4 * kCandCap * 8) +
-                                                       align_up((size_t)Bi * 4 * 4));
-            LGX_HIP_CHECK(hipMemsetAsync(ca.tile_flags, 0, (size_t)p.n_utiles * 4, stream));
             rc = launch_lds<false, kCandidates>(ca, p, stream, dtype);
-            if (rc) return rc;
-            ScoreArgs fb = a;  // the exact fallback: the running walk, unseeded, no floor, flagged tiles only
-            fb.floor = nullptr;
-            fb.tile_flags = ca.tile_flags;
-            rc = launch_lds<false>(fb, p, stream, dtype);
             if (rc) return rc;
             int32_t* oi = out_idx + R.u0 * k;
             float* ov = out_val ? out_val + R.u0 * k : nullptr;
-            const int64_t tu = (int64_t)p.waves * kUsersPerWave;
-            if (k <= 64) score_topk_cand_select<1><<<(unsigned)Bi, 64, 0, stream>>>(ca, tu, mask_value, apply_sigmoid, oi, ov);
-            else if (k <= 128) score_topk_cand_select<2><<<(unsigned)Bi, 64, 0, stream>>>(ca, tu, mask_value, apply_sigmoid, oi, ov);
-            else score_topk_cand_select<4><<<(unsigned)Bi, 64, 0, stream>>>(ca, tu, mask_value, apply_sigmoid, oi, ov);
+            if (k <= 64) score_topk_cand_select<1><<<(unsigned)Bi, 64, 0, stream>>>(ca, mask_value, apply_sigmoid, oi, ov);
+            else if (k <= 128) score_topk_cand_select<2><<<(unsigned)Bi, 64, 0, stream>>>(ca, mask_value, apply_sigmoid, oi, ov);
+            else score_topk_cand_select<4><<<(unsigned)Bi, 64, 0, stream>>>(ca, mask_value, apply_sigmoid, oi, ov);
             LGX_LAUNCH_CHECK();
             continue;
         } else if (seeded_sweep(p, mm, n_items, dtype)) {

@@ -209,12 +209,12 @@ def test_candidate_full_sweep_equals_one_sweep():
     assert (got >= kth - 1e-5 * kth.abs().clamp(min=1.0)).all()
 
 
-def test_candidate_overflow_takes_the_exact_fallback():
+def test_candidate_regions_compact_under_ties():
     """135,000 equal item rows after the floor window: a user whose score on that row reaches its
-    floor meets them all as candidates, overflows its regions, and its user tile is flagged and
-    recomputed by the running walk (the exact fallback); the other users' tiles keep the candidate
-    path, so both kinds of tile meet in one call.  The lists equal, as sets with their values, the
-    one-launch running walk's (ties at the k-th score broken by the lower item id in both)."""
+    floor meets them all as candidates; its regions run full and compact in place (their k best keys
+    kept, the threshold raised to the k-th key, ties broken by the lower item id) -- several times
+    over the sweep -- while the other users never compact.  The lists equal, as sets with their
+    values, the one-launch running walk's."""
     B, I, d, k = 256 * 256, 270_000, 64, 20
     plan = ops.score_topk_plan(B, I, d, torch.bfloat16, k)
     assert "candidates above score floors" in plan, plan
