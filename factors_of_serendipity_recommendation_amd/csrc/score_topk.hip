@@ -1443,6 +1443,7 @@ void score_topk_f32_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf)
 // epilogue.  d >= 192: the 32 users' rows take 96-128 VGPRs, two waves per SIMD spill (d=256: 72 B of
 // scratch), and a tile is 12-16 K MFMA cycles per wave against a ~1 K-cycle epilogue: 4 waves, one per
 // SIMD, every epilogue after the barrier.
+// (held to 128 VGPRs for two workgroups per CU, the d = 64 walk spills 112-140 B: one per CU)
 __host__ __device__ constexpr int walk_waves(int ks) { return ks <= 8 ? 8 : 4; }
 template <int KSTEPS, int MODE>
 __global__ __launch_bounds__(walk_waves(KSTEPS) * 64)
@@ -2044,7 +2045,7 @@ int launch_bf16_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t s
 template <int KS, bool MM, int MODE>
 int launch_f32_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     typedef LdsGeom<KS, kF32LdsWaves, 2, 4> G;
-    const size_t lists = (size_t)kF32LdsWaves * list_bytes_per_wave(a.k);
+    const size_t lists = MODE == kCandidates ? 0 : (size_t)kF32LdsWaves * list_bytes_per_wave(a.k);
     const int nbuf = lds_ring_buffers(G::TILE, lists, 1);
     const size_t shmem = (size_t)nbuf * G::TILE + lists;
     if (shmem > kLdsBytes) {
@@ -2063,23 +2064,15 @@ int launch_f32_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t st
 template <bool MM, int MODE = kTopK>
 int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream, int dtype = LGX_DTYPE_BF16) {
     const int ksteps = (int)(a.d / 16);
-    if constexpr (MODE == kFloorOnly || MODE == kCandidates) {
-        if (dtype == LGX_DTYPE_F32) {
-            set_error("lgx_score_topk: score floors and candidate sweeps are bf16 LDS kernel modes");
-            return LGX_ERR_UNSUPPORTED;
-        }
-    }
-    if constexpr (MODE != kFloorOnly && MODE != kCandidates) {
-        if (dtype == LGX_DTYPE_F32) {
-            switch (ksteps) {
-                case 4: return launch_f32_lds_kernel<4, MM, MODE>(a, p, stream);
-                case 8: return launch_f32_lds_kernel<8, MM, MODE>(a, p, stream);
-                case 12: return launch_f32_lds_kernel<12, MM, MODE>(a, p, stream);
-                case 16: return launch_f32_lds_kernel<16, MM, MODE>(a, p, stream);
-                default:
-                    set_error("lgx_score_topk: no f32 LDS kernel for d=%lld", (long long)a.d);
-                    return LGX_ERR_UNSUPPORTED;
-            }
+    if (dtype == LGX_DTYPE_F32) {
+        switch (ksteps) {
+            case 4: return launch_f32_lds_kernel<4, MM, MODE>(a, p, stream);
+            case 8: return launch_f32_lds_kernel<8, MM, MODE>(a, p, stream);
+            case 12: return launch_f32_lds_kernel<12, MM, MODE>(a, p, stream);
+            case 16: return launch_f32_lds_kernel<16, MM, MODE>(a, p, stream);
+            default:
+                set_error("lgx_score_topk: no f32 LDS kernel for d=%lld", (long long)a.d);
+                return LGX_ERR_UNSUPPORTED;
         }
     }
 #define LGX_SL(KS) return launch_bf16_lds_kernel<KS, MM, MODE>(a, p, stream)

@@ -396,8 +396,14 @@ def row_f4(rows, reps):
     def sel():
         _lib.check(L.lgx_strat_select(labels.data_ptr(), B, I, hist.data_ptr(), F + 1, tgt.data_ptr(), 77,
                                       out.data_ptr(), Kc, cnt.data_ptr(), st), "lgx_strat_select")
+    def fused20():  # > 16 folds: the labels alone in the walk, the counts by a separate pass
+        _lib.check(L.lgx_strat_labels_fused(eu.data_ptr(), None, ei.data_ptr(), B, I, d, _lib.LGX_DTYPE_F32, min16,
+                                            inter16, 20, mp.data_ptr(), mi.data_ptr(), labels.data_ptr(),
+                                            hist20.data_ptr(), st), "lgx_strat_labels_fused")
+    hist20 = torch.empty((B, 21), dtype=torch.int32, device=DEV)
     ms_s = gpu_ms(lambda: ops.score_dense(eu, ei), reps)
     ms_l = gpu_ms(lab, reps)
+    ms_f20 = gpu_ms(fused20, reps)
     ms_f = gpu_ms(fused, reps)
     ms_h = gpu_ms(hist_only, reps)
     fused()
@@ -411,7 +417,8 @@ def row_f4(rows, reps):
          n * I, s, f"{n} users x {I} items: numpy dot + float16 labels + histograms (labels only)", 1,
          f"per batch: fused labels + counts {ms_f:.2f} ms (the counting pass over the labels it replaces: "
          f"{ms_h:.2f} ms), select "
-         f"{ms_p:.2f} ms; the two-step path: score_dense {ms_s:.2f} + labels {ms_l:.2f} ms; roofline: the "
+         f"{ms_p:.2f} ms; 20 folds (labels in the walk, counts by a separate pass) {ms_f20:.2f} ms; "
+         f"the two-step path: score_dense {ms_s:.2f} + labels {ms_l:.2f} ms; roofline: the "
          "fused kernel's f32 MFMA flops over the whole batch time")
     del S, labels
     torch.cuda.empty_cache()
