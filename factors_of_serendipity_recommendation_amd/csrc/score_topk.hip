@@ -8,20 +8,21 @@
 // (recommend.py:163-164, :375-377).  The reference materialises the [B, I] rating matrix; here it
 // never leaves the accumulators.
 //
-// MI355X design:
-//   * one 256-thread workgroup = 4 waves x 32 query users; a wave keeps its 32 users' embedding
-//     fragments in VGPRs for the whole sweep and walks 32-item tiles of its item split;
-//   * items are the MFMA A operand and users the B operand, so each lane ends a tile holding 16
-//     item scores of ONE user: the top-k filter is one compare per score against a per-lane
-//     threshold (the user's current k-th best), and only survivors (~k ln(I/k) per user over the
-//     whole catalog) take the slow path (mask lookup + sorted insertion into the user's list in
-//     LDS);
-//   * bf16: v_mfma_f32_32x32x16_bf16 (fragments are plain 16-B loads); fp32 parity path:
-//     v_mfma_f32_32x32x2_f32 (exact fp32 fmaf chain) with the reduction index permuted so each
-//     lane still loads 16-B chunks;
-//   * small query batches split the catalog over workgroups (grid.y); every split writes its
-//     sorted partial list and a one-wave-per-user merge (register bitonic network) finishes, adds
-//     the masked tail when fewer than k unmasked items exist, applies the optional sigmoid.
+// MI355X design (one file, four kernel families):
+//   * score_topk_bf16_lds / score_topk_f32_lds -- the LDS-ring walk: a workgroup keeps its users'
+//     rows in VGPRs (the MFMA B operand) and streams 64-item tiles of the catalog (the A operand)
+//     through an LDS ring filled by LDS-DMA; v_mfma_f32_16x16x32_bf16 / 16x16x4_f32.  Its modes:
+//     the running top-k with the mask (kTopK), the global min / max (kMinMaxOnly), the per-user score
+//     floors (kFloorOnly), and the candidate sweep (kCandidates: every score at or above its user's
+//     floor appended to HBM, the exact top-k per user afterwards by score_topk_cand_select) which
+//     the bf16 full-catalog sweeps use;
+//   * score_walk_f32_lds -- the same walk's dense modes: fp32 getUsersRating scores and the
+//     stratification labels of recommend.py:375-381, bit for bit the same f32 sums;
+//   * score_topk_kernel -- a register-fragment walk for the shapes the LDS walk does not cover, and
+//     score_dense_lds / strat_label_lds for the bf16 dense scores and labels;
+//   * score_topk_finalize / score_topk_cand_select -- one wave per user merges split lists or
+//     candidate keys (register bitonic network), adds the masked tail when fewer than k unmasked
+//     items exist and applies the optional sigmoid.
 #include <algorithm>
 #include <type_traits>
 #include <cmath>
@@ -797,17 +798,51 @@ __device__ __forceinline__ void lds_dma16(const void* sbase, uint32_t voff, uint
 }
 #pragma clang diagnostic pop
 
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n (conservative above 15)
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n; the counter has 6 bits, but the walks that issue
+// no stores inside the ring loop keep the 15-entry switch (conservative above 15: the larger jump
+// table costs the register-tight top-k bodies a spill)
+template <bool WIDE = false>
 __device__ __forceinline__ void wait_vmcnt_le(int n) {
 #define LGX_VMW(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-    switch (n) {
-        LGX_VMW(1) LGX_VMW(2) LGX_VMW(3) LGX_VMW(4) LGX_VMW(5) LGX_VMW(6) LGX_VMW(7) LGX_VMW(8)
-        LGX_VMW(9) LGX_VMW(10) LGX_VMW(11) LGX_VMW(12) LGX_VMW(13) LGX_VMW(14) LGX_VMW(15)
-        default:
-            if (n >= 16) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!WIDE || n <= 15) {
+        switch (n) {
+            LGX_VMW(1) LGX_VMW(2) LGX_VMW(3) LGX_VMW(4) LGX_VMW(5) LGX_VMW(6) LGX_VMW(7) LGX_VMW(8) LGX_VMW(9) LGX_VMW(10) LGX_VMW(11) LGX_VMW(12) LGX_VMW(13) LGX_VMW(14) LGX_VMW(15)
+            default:
+                if (n >= 16) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    } else {
+        switch (n) {
+            LGX_VMW(16) LGX_VMW(17) LGX_VMW(18) LGX_VMW(19) LGX_VMW(20) LGX_VMW(21) LGX_VMW(22) LGX_VMW(23)
+             LGX_VMW(24) LGX_VMW(25) LGX_VMW(26) LGX_VMW(27) LGX_VMW(28) LGX_VMW(29) LGX_VMW(30) LGX_VMW(31)
+             LGX_VMW(32) LGX_VMW(33) LGX_VMW(34) LGX_VMW(35) LGX_VMW(36) LGX_VMW(37) LGX_VMW(38) LGX_VMW(39)
+             LGX_VMW(40) LGX_VMW(41) LGX_VMW(42) LGX_VMW(43) LGX_VMW(44) LGX_VMW(45) LGX_VMW(46) LGX_VMW(47)
+             LGX_VMW(48) LGX_VMW(49) LGX_VMW(50) LGX_VMW(51) LGX_VMW(52) LGX_VMW(53) LGX_VMW(54) LGX_VMW(55)
+             LGX_VMW(56) LGX_VMW(57) LGX_VMW(58) LGX_VMW(59) LGX_VMW(60) LGX_VMW(61) LGX_VMW(62) LGX_VMW(63)
+            
+            default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+        }
     }
 #undef LGX_VMW
+}
+
+// Global stores the LDS walk counts itself: one instruction each, never merged, dropped or
+// predicated away by the compiler.  vmcnt counts loads, stores and LDS-DMA together and retires them
+// in issue order, so every store issued after the refill a wait is for must be allowed for in that
+// wait, or the wait also waits for the newest refills; an epilogue reports the stores it issued
+// (a lane with nothing to store writes to g_store_sink instead, so the count stays wave-uniform).
+__device__ uint4 g_store_sink[4];
+__device__ __forceinline__ void st_u8(void* p, uint32_t v) {
+    asm volatile("global_store_byte %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_u32(void* p, uint32_t v) {
+    asm volatile("global_store_dword %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_u64(void* p, uint64_t v) {
+    asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_u128(void* p, u32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
 }
 
 __device__ __forceinline__ uint32_t lds_u32(const void* p) {
@@ -1000,8 +1035,9 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         if (cuB < a.B) thrB = make_key(a.floor[cuB * a.n_splits + split], 0x7fffffff);
         tauA = key_score(thrA);
         tauB = key_score(thrB);
-        candA = a.cand + ((size_t)(cuA < a.B ? cuA : 0) * 4 + q4) * a.cand_cap;
-        candB = a.cand + ((size_t)(cuB < a.B ? cuB : 0) * 4 + q4) * a.cand_cap;
+        // padding users never pass (threshold ~0), and their stores go to the sink
+        candA = cuA < a.B ? a.cand + ((size_t)cuA * 4 + q4) * a.cand_cap : reinterpret_cast<uint64_t*>(g_store_sink);
+        candB = cuB < a.B ? a.cand + ((size_t)cuB * 4 + q4) * a.cand_cap : reinterpret_cast<uint64_t*>(g_store_sink);
     }
     // regroup: swap(X = user block 0, Y = user block 1) between rows 2m and 2m+1 (lanes l, l^16)
     // leaves X' = items 16 ib + 8 h + reg, Y' = items 16 ib + 8 h + 4 + reg of user l & 31
@@ -1122,37 +1158,64 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
             }
     };
     // dense modes: lane (q4, r16) holds items e0 + 16 ib + 4 q4 + 0..3 of user 16 ub + r16
+    // counted stores of the current iteration / a drain (vmcnt(0)) taken by an epilogue
+    int vm_stores = 0;
+    bool vm_drained = false;
+    auto drain_stores = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        vm_drained = true;
+        vm_stores = 0;
+    };
+    // whole tiles: 8 counted 16-B stores per wave (32 4-B stores when rows are not 16-B aligned),
+    // padding users' lanes into the sink; the split's partial last tile: plain stores, then a drain
     auto dense_tile = [&](int64_t e0) {
         const int64_t rem = i_end - e0;  // items of the tile inside the split
+        const bool whole = rem >= G::TILE_ITEMS;  // wave-uniform
 #pragma unroll
         for (int ub = 0; ub < 2; ++ub) {
             const int64_t bu = utile * G::USERS + wave * kUsersPerWave + 16 * ub + r16;
-            if (bu >= a.B) continue;
-            float* row = o.scores + bu * a.n_items + e0;
+            const bool uok = bu < a.B;
+            float* row = o.scores + (uok ? bu : 0) * a.n_items + e0;
 #pragma unroll
             for (int ib = 0; ib < 4; ++ib) {
                 const int off = 16 * ib + 4 * q4;
                 float v[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = MODE == kDenseSigmoid ? fast_sigmoid(c[ub][ib][r]) : c[ub][ib][r];
-                if (o.vec4 && off + 4 <= rem) {
-                    *reinterpret_cast<float4*>(row + off) = make_float4(v[0], v[1], v[2], v[3]);
-                } else {
+                if (whole && o.vec4) {
+                    st_u128(uok ? static_cast<void*>(row + off) : static_cast<void*>(g_store_sink),
+                            u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                                  __float_as_uint(v[3])});
+                } else if (whole) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        if (off + r < rem) row[off + r] = v[r];
+                        st_u32(uok ? static_cast<void*>(row + off + r) : static_cast<void*>(g_store_sink),
+                               __float_as_uint(v[r]));
+                } else if (uok) {
+                    if (o.vec4 && off + 4 <= rem) {
+                        *reinterpret_cast<float4*>(row + off) = make_float4(v[0], v[1], v[2], v[3]);
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            if (off + r < rem) row[off + r] = v[r];
+                    }
                 }
             }
         }
+        if (whole) vm_stores += o.vec4 ? 8 : 32;
+        else drain_stores();
     };
+    // labels: the same store accounting as dense_tile (8 counted 4-B stores per whole tile, 32 1-B
+    // stores when rows are not 4-B aligned)
     auto label_tile = [&](auto est_tag, int64_t e0) {
         constexpr bool EST1 = decltype(est_tag)::value;
         const int64_t rem = i_end - e0;
+        const bool whole = rem >= G::TILE_ITEMS;  // wave-uniform
 #pragma unroll
         for (int ub = 0; ub < 2; ++ub) {
             const int64_t bu = utile * G::USERS + wave * kUsersPerWave + 16 * ub + r16;
-            if (bu >= a.B) continue;
-            int8_t* row = o.labels + bu * a.n_items + e0;
+            const bool uok = bu < a.B;
+            int8_t* row = o.labels + (uok ? bu : 0) * a.n_items + e0;
             uint32_t* hu = hc + (wave * kUsersPerWave + 16 * ub + r16) * kHistStride;
 #pragma unroll
             for (int ib = 0; ib < 4; ++ib) {
@@ -1160,27 +1223,38 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
                 uint32_t l[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) l[r] = strat_label_of<EST1>(c[ub][ib][r], o.thr, T, TP);
-                if (o.hist) {
+                if (o.hist && uok) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
                         if (off + r < rem) atomicAdd(hu + l[r], 1u);
                 }
                 const uint32_t w = l[0] | (l[1] << 8) | (l[2] << 16) | (l[3] << 24);
-                if (o.vec4 && off + 4 <= rem) {
-                    *reinterpret_cast<uint32_t*>(row + off) = w;
-                } else {
+                if (whole && o.vec4) {
+                    st_u32(uok ? static_cast<void*>(row + off) : static_cast<void*>(g_store_sink), w);
+                } else if (whole) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        if (off + r < rem) row[off + r] = (int8_t)((w >> (8 * r)) & 255);
+                        st_u8(uok ? static_cast<void*>(row + off + r) : static_cast<void*>(g_store_sink),
+                              (w >> (8 * r)) & 255);
+                } else if (uok) {
+                    if (o.vec4 && off + 4 <= rem) {
+                        *reinterpret_cast<uint32_t*>(row + off) = w;
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            if (off + r < rem) row[off + r] = (int8_t)((w >> (8 * r)) & 255);
+                    }
                 }
             }
         }
+        if (whole) vm_stores += o.vec4 ? 8 : 32;
+        else drain_stores();
     };
     // kCandidates, lane-local and rare: the region's k best keys to its front (partial selection sort
     // over its n keys, read back at device scope after this lane's stores have completed); returns
     // the k-th best key, the region's new threshold
     auto compact = [&](uint64_t* reg, int n) -> uint64_t {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this lane's stores (and the refills) done
         for (int j = 0; j < k; ++j) {
             uint64_t m = 0;
             int at = j;
@@ -1196,7 +1270,10 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
                 __hip_atomic_store(reg + at, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(reg + j, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            if (j + 1 == k) return m;
+            if (j + 1 == k) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                return m;
+            }
         }
         return 0ull;
     };
@@ -1220,15 +1297,21 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
             const float a0 = fmaxf(fmaxf(c[0][ib][0], c[0][ib][1]), fmaxf(c[0][ib][2], c[0][ib][3]));
             const float a1 = fmaxf(fmaxf(c[1][ib][0], c[1][ib][1]), fmaxf(c[1][ib][2], c[1][ib][3]));
             if (__ballot((a0 >= tauA) | (a1 >= tauB)) == 0ull) continue;  // no candidate in this item block
+            // every lane stores (8 counted stores per flagged block); a key that does not pass lands in
+            // the slot the next candidate overwrites (cnt <= cap - 1 at every store: a region is
+            // compacted once it holds more than cap - 16, and a tile brings at most 16 per region)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int off = 16 * ib + 4 * q4 + r;
                 const int32_t item = (int32_t)(e0 + off);
                 const bool in = off < rem;
                 const uint64_t k0 = make_key(c[0][ib][r], item), k1 = make_key(c[1][ib][r], item);
-                if (in && k0 >= thrA) candA[cntA++] = k0;
-                if (in && k1 >= thrB) candB[cntB++] = k1;
+                st_u64(candA + cntA, k0);
+                cntA += in && k0 >= thrA ? 1 : 0;
+                st_u64(candB + cntB, k1);
+                cntB += in && k1 >= thrB ? 1 : 0;
             }
+            vm_stores += 8;
         }
         const int lim = a.cand_cap - 16;
         if (__ballot(cntA > lim || cntB > lim) != 0ull) {  // rare: some region is nearly full
@@ -1242,6 +1325,8 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
                 cntB = k;
                 tauB = key_score(thrB);
             }
+            vm_drained = true;  // compact() ended on vmcnt(0) in the lanes that ran it: the wave's
+            vm_stores = 0;      // counter is empty (other lanes waited at the same instructions)
         }
     };
     auto epilogue = [&](int64_t e0) {
@@ -1323,15 +1408,26 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         // candidates, and skip the two cross-lane reads
         if (SKIP && __ballot(st.tau != tau_before) != 0ull) refresh_taus();
     };
+    // counted stores of iterations t-2, t-1, t (the refill of tile t+1 was issued at the start of
+    // iteration t+1-ahead, ahead <= 3: every store of those iterations is younger than it)
+    int vs0 = 0, vs1 = 0;
     for (int64_t t = 0; t < ntiles; ++t) {
         const int64_t t0 = tile_start(t);
+        vm_stores = 0;
+        vm_drained = false;
         if (t + ahead < ntiles) stage(sbuf, tile_start(t + ahead));
         if (late && t > 0) epilogue(prev_t0);
         compute();
         if (!late) epilogue(t0);
         prev_t0 = t0;
-        // tiles t+2 .. t+ahead may stay in flight; tile t+1 must have landed
-        wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(t + ahead, ntiles - 1) - (t + 1)));
+        if (vm_drained) vs0 = vs1 = 0;  // a drain retired everything issued before it
+        const int younger = vm_stores + (ahead >= 2 ? vs1 : 0) + (ahead >= 3 ? vs0 : 0);
+        vs0 = vs1;
+        vs1 = vm_stores;
+        // tiles t+2 .. t+ahead and the stores issued since tile t+1's refill may stay in flight;
+        // tile t+1 must have landed
+        wait_vmcnt_le<MODE == kCandidates || dense_mode(MODE)>(
+            my_pieces * (int)max<int64_t>(0, min<int64_t>(t + ahead, ntiles - 1) - (t + 1)) + younger);
         __syncthreads();
         buf = buf + 1 == nbuf ? 0 : buf + 1;
         sbuf = sbuf + 1 == nbuf ? 0 : sbuf + 1;
