@@ -13,16 +13,13 @@
 //     rows in VGPRs (the MFMA B operand) and streams 64-item tiles of the catalog (the A operand)
 //     through an LDS ring filled by LDS-DMA; v_mfma_f32_16x16x32_bf16 / 16x16x4_f32.  Its modes:
 //     the running top-k with the mask (kTopK), the global min / max (kMinMaxOnly), the per-user score
-//     floors (kFloorOnly), and the candidate sweep (kCandidates: every score at or above its user's
-//     floor appended to HBM, the exact top-k per user afterwards by score_topk_cand_select) which
-//     the bf16 full-catalog sweeps use;
+//     floors (kFloorOnly) that start an unseeded sweep's lists;
 //   * score_walk_f32_lds -- the same walk's dense modes: fp32 getUsersRating scores and the
 //     stratification labels of recommend.py:375-381, bit for bit the same f32 sums;
 //   * score_topk_kernel -- a register-fragment walk for the shapes the LDS walk does not cover, and
 //     score_dense_lds / strat_label_lds for the bf16 dense scores and labels;
-//   * score_topk_finalize / score_topk_cand_select -- one wave per user merges split lists or
-//     candidate keys (register bitonic network), adds the masked tail when fewer than k unmasked
-//     items exist and applies the optional sigmoid.
+//   * score_topk_finalize -- one wave per user merges split lists (register bitonic network), adds
+//     the masked tail when fewer than k unmasked items exist and applies the optional sigmoid.
 #include <algorithm>
 #include <type_traits>
 #include <cmath>
@@ -106,12 +103,6 @@ struct ScoreArgs {
     // floor_items items of each split, read by an unseeded sweep as every list's starting threshold
     float* floor;
     int64_t floor_items;
-    // candidate sweep (kCandidates): every key at or above its lane's threshold is appended to
-    // cand[(b * 4 + q4) * cand_cap + n] (the 4 lanes of user b in the MFMA layout own a region each;
-    // cand_cnt[b * 4 + q4] = the final n)
-    uint64_t* cand;
-    int32_t* cand_cnt;
-    int cand_cap;
 };
 
 // Candidates whose mask test the Bloom filter cannot settle ("suspects", ~10 % of the survivors) are
@@ -715,15 +706,6 @@ constexpr int kDenseScores = 3;
 constexpr int kDenseSigmoid = 4;
 constexpr int kStratLabels = 5;
 __host__ __device__ constexpr bool dense_mode(int m) { return m == kDenseScores || m == kDenseSigmoid || m == kStratLabels; }
-// kCandidates: the sweep without a running top-k in LDS.  Each lane of a user (4 per user in the MFMA
-// layout, each seeing a quarter of the items) appends every key at or above its threshold to its own
-// region in HBM (fire-and-forget stores; no LDS lists, no drains, no Bloom filter: the mask and the
-// exact top-k are applied per user afterwards by score_topk_cand_select).  The threshold starts at
-// the user's score floor (a lower bound of its k-th best, kFloorOnly): ~1,450 candidates per user at
-// I = 1M, ~360 per region.  A region about to run full is compacted in place to its own k best keys
-// and its threshold raised to the k-th of them -- valid because a key of the user's top-k is in the
-// top-k of its own region -- so no region ever overflows, whatever the data (ties included).
-constexpr int kCandidates = 6;
 
 struct StratThr {
     float t[32];
@@ -838,9 +820,6 @@ __device__ __forceinline__ void st_u8(void* p, uint32_t v) {
 __device__ __forceinline__ void st_u32(void* p, uint32_t v) {
     asm volatile("global_store_dword %0, %1, off" ::"v"(p), "v"(v) : "memory");
 }
-__device__ __forceinline__ void st_u64(void* p, uint64_t v) {
-    asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(v) : "memory");
-}
 __device__ __forceinline__ void st_u128(void* p, u32x4 v) {
     asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
 }
@@ -942,12 +921,10 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     }
     TopK st;
     st.init(lk, lk + list_keys_per_wave(k), k, lane, b, user_ok);
-    if constexpr (MODE != kCandidates) {
-        st.enable_suspects(a);
-        st.build_bloom(a);
-        if (a.seed_score) st.seed(a);
-        else if (MODE != kFloorOnly && a.floor && user_ok) st.tau = a.floor[b * a.n_splits + split];
-    }
+    st.enable_suspects(a);
+    st.build_bloom(a);
+    if (a.seed_score) st.seed(a);
+    else if (MODE != kFloorOnly && a.floor && user_ok) st.tau = a.floor[b * a.n_splits + split];
     // consume the prologue loads here: otherwise the compiler treats them as possibly pending at
     // the loop header and waits vmcnt(0) -- i.e. for the tile prefetch -- in every iteration
 #pragma unroll
@@ -1022,23 +999,6 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         tauB = __shfl(st.tau, 16 + (lane & 15));
     };
     if (SKIP) refresh_taus();
-    // kCandidates: this lane's two users (16 ub + r16) -- key thresholds (tauA / tauB: their scores,
-    // for the fast path), candidate counts, regions
-    const int64_t cuA = utile * G::USERS + wave * kUsersPerWave + r16, cuB = cuA + 16;
-    int cntA = 0, cntB = 0;
-    uint64_t thrA = ~0ull, thrB = ~0ull;  // padding users: nothing passes
-    uint64_t* candA = nullptr;
-    uint64_t* candB = nullptr;
-    if constexpr (MODE == kCandidates) {
-        // the floor key of the lowest rank: every score >= the floor passes, ties included
-        if (cuA < a.B) thrA = make_key(a.floor[cuA * a.n_splits + split], 0x7fffffff);
-        if (cuB < a.B) thrB = make_key(a.floor[cuB * a.n_splits + split], 0x7fffffff);
-        tauA = key_score(thrA);
-        tauB = key_score(thrB);
-        // padding users never pass (threshold ~0), and their stores go to the sink
-        candA = cuA < a.B ? a.cand + ((size_t)cuA * 4 + q4) * a.cand_cap : reinterpret_cast<uint64_t*>(g_store_sink);
-        candB = cuB < a.B ? a.cand + ((size_t)cuB * 4 + q4) * a.cand_cap : reinterpret_cast<uint64_t*>(g_store_sink);
-    }
     // regroup: swap(X = user block 0, Y = user block 1) between rows 2m and 2m+1 (lanes l, l^16)
     // leaves X' = items 16 ib + 8 h + reg, Y' = items 16 ib + 8 h + 4 + reg of user l & 31
     auto regroup = [&]() {
@@ -1250,90 +1210,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         if (whole) vm_stores += o.vec4 ? 8 : 32;
         else drain_stores();
     };
-    // kCandidates, lane-local and rare: the region's k best keys to its front (partial selection sort
-    // over its n keys, read back at device scope after this lane's stores have completed); returns
-    // the k-th best key, the region's new threshold
-    auto compact = [&](uint64_t* reg, int n) -> uint64_t {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this lane's stores (and the refills) done
-        for (int j = 0; j < k; ++j) {
-            uint64_t m = 0;
-            int at = j;
-            for (int i = j; i < n; ++i) {
-                const uint64_t x = __hip_atomic_load(reg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (x > m) {
-                    m = x;
-                    at = i;
-                }
-            }
-            if (at != j) {
-                const uint64_t y = __hip_atomic_load(reg + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(reg + at, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(reg + j, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (j + 1 == k) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                return m;
-            }
-        }
-        return 0ull;
-    };
-    // kCandidates: lane (q4, r16) holds items e0 + 16 ib + 4 q4 + reg of users cuA (c[0]) and cuB (c[1]);
-    // a tile appends at most 16 keys per region, so a region is compacted once it holds more than
-    // cap - 16
-    auto cand_tile = [&](int64_t e0) {
-        const bool tail = e0 + G::TILE_ITEMS > i_end;
-        float m0 = c[0][0][0], m1 = c[1][0][0];
-#pragma unroll
-        for (int ib = 0; ib < 4; ++ib)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                m0 = fmaxf(m0, c[0][ib][r]);
-                m1 = fmaxf(m1, c[1][ib][r]);
-            }
-        if (__ballot((m0 >= tauA) | (m1 >= tauB)) == 0ull) return;  // wave-uniform fast path
-        const int32_t rem = tail ? (int32_t)(i_end - e0) : G::TILE_ITEMS;
-#pragma unroll
-        for (int ib = 0; ib < 4; ++ib) {
-            const float a0 = fmaxf(fmaxf(c[0][ib][0], c[0][ib][1]), fmaxf(c[0][ib][2], c[0][ib][3]));
-            const float a1 = fmaxf(fmaxf(c[1][ib][0], c[1][ib][1]), fmaxf(c[1][ib][2], c[1][ib][3]));
-            if (__ballot((a0 >= tauA) | (a1 >= tauB)) == 0ull) continue;  // no candidate in this item block
-            // every lane stores (8 counted stores per flagged block); a key that does not pass lands in
-            // the slot the next candidate overwrites (cnt <= cap - 1 at every store: a region is
-            // compacted once it holds more than cap - 16, and a tile brings at most 16 per region)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int off = 16 * ib + 4 * q4 + r;
-                const int32_t item = (int32_t)(e0 + off);
-                const bool in = off < rem;
-                const uint64_t k0 = make_key(c[0][ib][r], item), k1 = make_key(c[1][ib][r], item);
-                st_u64(candA + cntA, k0);
-                cntA += in && k0 >= thrA ? 1 : 0;
-                st_u64(candB + cntB, k1);
-                cntB += in && k1 >= thrB ? 1 : 0;
-            }
-            vm_stores += 8;
-        }
-        const int lim = a.cand_cap - 16;
-        if (__ballot(cntA > lim || cntB > lim) != 0ull) {  // rare: some region is nearly full
-            if (cntA > lim) {
-                thrA = compact(candA, cntA);
-                cntA = k;
-                tauA = key_score(thrA);
-            }
-            if (cntB > lim) {
-                thrB = compact(candB, cntB);
-                cntB = k;
-                tauB = key_score(thrB);
-            }
-            vm_drained = true;  // compact() ended on vmcnt(0) in the lanes that ran it: the wave's
-            vm_stores = 0;      // counter is empty (other lanes waited at the same instructions)
-        }
-    };
     auto epilogue = [&](int64_t e0) {
-        if constexpr (MODE == kCandidates) {
-            cand_tile(e0);
-            return;
-        }
         if constexpr (MODE == kDenseScores || MODE == kDenseSigmoid) {
             dense_tile(e0);
             return;
@@ -1426,7 +1303,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         vs1 = vm_stores;
         // tiles t+2 .. t+ahead and the stores issued since tile t+1's refill may stay in flight;
         // tile t+1 must have landed
-        wait_vmcnt_le<MODE == kCandidates || dense_mode(MODE)>(
+        wait_vmcnt_le<dense_mode(MODE)>(
             my_pieces * (int)max<int64_t>(0, min<int64_t>(t + ahead, ntiles - 1) - (t + 1)) + younger);
         __syncthreads();
         buf = buf + 1 == nbuf ? 0 : buf + 1;
@@ -1446,11 +1323,6 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         return;
     }
     if constexpr (MODE == kDenseScores || MODE == kDenseSigmoid) return;
-    if constexpr (MODE == kCandidates) {
-        if (cuA < a.B) a.cand_cnt[cuA * 4 + q4] = cntA;
-        if (cuB < a.B) a.cand_cnt[cuB * 4 + q4] = cntB;
-        return;
-    }
     if constexpr (MODE == kMinMaxOnly) {
 #pragma unroll
         for (int m = 32; m > 0; m >>= 1) {
@@ -1617,34 +1489,6 @@ __global__ __launch_bounds__(64) void score_topk_finalize(ScoreArgs a, float mas
         minmax_out[0] = unord_f32(a.minmax[0]);
         minmax_out[1] = unord_f32(a.minmax[1]);
     }
-}
-
-// kCandidates' second half, one wave per query: the exact top-k of the user's candidate keys, masked
-// items dropped -- tested only for keys above the running k-th best, ~k ln(n / k) of them -- in the
-// same key order (score, then the lower index) as the running walk, so the lists are its lists.
-template <int R>
-__global__ __launch_bounds__(64) void score_topk_cand_select(ScoreArgs a, float mask_value, int apply_sigmoid,
-                                                             int32_t* __restrict__ out_idx,
-                                                             float* __restrict__ out_val) {
-    const int lane = threadIdx.x;
-    const int64_t b = blockIdx.x;
-    const int k = a.k;
-    WaveList<R> top;
-    top.clear();
-    {
-        for (int q = 0; q < 4; ++q) {
-            const int n = min(a.cand_cnt[b * 4 + q], a.cand_cap);
-            const uint64_t* src = a.cand + ((size_t)b * 4 + q) * a.cand_cap;
-            for (int base = 0; base < n; base += 64) {
-                const int j = base + lane;
-                uint64_t key = j < n ? src[j] : 0ull;
-                const uint64_t thr = top.at(k - 1);  // all lanes (a shuffle)
-                if (a.mask_indptr && key > thr && is_masked(a, b, key_index(key))) key = 0ull;
-                top.push(key, k, lane);
-            }
-        }
-    }
-    emit_topk(top, a, b, lane, mask_value, apply_sigmoid, out_idx, out_val);
 }
 
 __global__ void minmax_init(uint32_t* mm) {
@@ -2126,7 +1970,7 @@ template <int KS, bool MM, int MODE>
 int launch_bf16_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     typedef LdsGeom<KS, kBf16LdsWaves, 2> G;
     // the candidate sweep keeps no lists in LDS: the ring takes it (4 tiles at d = 256)
-    const size_t lists = MODE == kCandidates ? 0 : (size_t)kBf16LdsWaves * list_bytes_per_wave(a.k, kPendBf16Lds);
+    const size_t lists = (size_t)kBf16LdsWaves * list_bytes_per_wave(a.k, kPendBf16Lds);
     const int nbuf = lds_ring_buffers(G::TILE, lists, 1);
     const size_t shmem = (size_t)nbuf * G::TILE + lists;
     int rc = set_lds_limit(score_topk_bf16_lds<KS, MM, MODE>, shmem);
@@ -2141,7 +1985,7 @@ int launch_bf16_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t s
 template <int KS, bool MM, int MODE>
 int launch_f32_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     typedef LdsGeom<KS, kF32LdsWaves, 2, 4> G;
-    const size_t lists = MODE == kCandidates ? 0 : (size_t)kF32LdsWaves * list_bytes_per_wave(a.k);
+    const size_t lists = (size_t)kF32LdsWaves * list_bytes_per_wave(a.k);
     const int nbuf = lds_ring_buffers(G::TILE, lists, 1);
     const size_t shmem = (size_t)nbuf * G::TILE + lists;
     if (shmem > kLdsBytes) {
@@ -2252,21 +2096,8 @@ size_t range_susp_bytes(const UserRange& r) {
 }
 // the LDS kernel's score floors [users, n_splits]
 size_t range_floor_bytes(const UserRange& r) { return r.p.lds ? align_up((size_t)(r.u1 - r.u0) * r.p.n_splits * 4) : 0; }
-// the candidate sweep (kCandidates + score_topk_cand_select): bf16 full sweeps of >= 256 K items.
-// Candidate regions of kCandCap keys per user and lane (16 KB per user): floors over 16 384 items
-// leave ~1,450 candidates per user at 1 M items, ~360 per region; the floor's own spread puts a few
-// percent of the regions past the cap, which then compact in place (kCandidates).
-constexpr int kCandCap = 512;
-inline bool cand_sweep(const SplitPlan& p, bool minmax, int dtype, int64_t n_items) {
-    return p.lds && p.n_splits == 1 && !minmax && dtype == LGX_DTYPE_BF16 && n_items >= 16 * 16384;
-}
-size_t range_cand_bytes(const UserRange& r, int dtype, int64_t n_items) {
-    if (!cand_sweep(r.p, false, dtype, n_items)) return 0;
-    const int64_t n = r.u1 - r.u0;
-    return align_up((size_t)n * 4 * kCandCap * 8) + align_up((size_t)n * 4 * 4);
-}
-size_t range_ws_bytes(const UserRange& r, int k, int dtype, int64_t n_items) {
-    return 2 * range_list_bytes(r, k) + range_susp_bytes(r) + range_floor_bytes(r) + range_cand_bytes(r, dtype, n_items);
+size_t range_ws_bytes(const UserRange& r, int k) {
+    return 2 * range_list_bytes(r, k) + range_susp_bytes(r) + range_floor_bytes(r);
 }
 
 int plan_ranges(int64_t B, int64_t n_items, int dtype, int64_t d, int k, UserRange* r) {
@@ -2284,7 +2115,7 @@ int plan_ranges(int64_t B, int64_t n_items, int dtype, int64_t d, int k, UserRan
     if (full < B) r[n++] = {full, B, plan_splits(B - full, n_items, dtype, d, k), 0};
     for (int i = 0; i < n; ++i) {
         r[i].ws_off = off;
-        off += range_ws_bytes(r[i], k, dtype, n_items);
+        off += range_ws_bytes(r[i], k);
     }
     return n;
 }
@@ -2298,8 +2129,8 @@ int plan_ranges(int64_t B, int64_t n_items, int dtype, int64_t d, int k, UserRan
 // sweep 463.7 ms, these 7 stages 431.9 ms (-6.9 %); 2 stages -2 %, 3 stages -4 %
 // (profiles/r02_score_lab_seeded.txt, profiles/r02_score_lab_stages.txt).
 constexpr int64_t kSeedItems = 16384;
-inline bool seeded_sweep(const SplitPlan& p, bool minmax, int64_t n_items, int dtype) {
-    return p.lds && p.n_splits == 1 && !minmax && n_items >= 16 * kSeedItems && !cand_sweep(p, minmax, dtype, n_items);
+inline bool seeded_sweep(const SplitPlan& p, bool minmax, int64_t n_items) {
+    return p.lds && p.n_splits == 1 && !minmax && n_items >= 16 * kSeedItems;
 }
 // Score floors (kFloorOnly): an unseeded LDS sweep -- the first stage of a seeded sweep, or every
 // split of a split launch -- starts its lists at a floor taken from its first kFloorItems items
@@ -2320,7 +2151,7 @@ size_t topk_ws_bytes(int64_t B, int64_t n_items, int k, int dtype, int64_t d) {
     UserRange r[2];
     const int n = plan_ranges(B, n_items, dtype, d, k, r);
     size_t bytes = 0;
-    for (int i = 0; i < n; ++i) bytes += range_ws_bytes(r[i], k, dtype, n_items);
+    for (int i = 0; i < n; ++i) bytes += range_ws_bytes(r[i], k);
     return bytes + 512;  // + the global min / max words
 }
 
@@ -2354,8 +2185,7 @@ extern "C" int lgx_score_topk_plan(int64_t B, int64_t n_items, int64_t d, int dt
                                  : (v1_waves(k) == 4 ? "score_topk_kernel<4 waves>" : "score_topk_kernel<1 wave>");
         const char* mode = p.lds ? (p.n_splits == 1 ? "full-sweep" : (p.xcd_affine ? "split-xcd" : "split"))
                                  : "split";
-        const char* how = seeded_sweep(p, false, n_items, dtype) ? " (seeded in stages)"
-                          : cand_sweep(p, false, dtype, n_items) ? " (candidates above score floors)" : "";
+        const char* how = seeded_sweep(p, false, n_items) ? " (seeded in stages)" : "";
         off += snprintf(buf + off, len - off, "%s%s users[%lld,%lld) %s%s n_splits=%d utiles=%lld",
                         i ? "; " : "", kern, (long long)r[i].u0, (long long)r[i].u1, mode, how, p.n_splits,
                         (long long)p.n_utiles);
@@ -2409,24 +2239,7 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
             rc = launch_lds<false, kFloorOnly>(a, p, stream, dtype);
             if (rc) return rc;
         }
-        if (cand_sweep(p, mm, dtype, n_items)) {
-            // floors (above) -> every key at or above its lane's threshold into the candidate regions ->
-            // the per-user exact top-k of the unmasked candidates
-            char* cb = wsr + 2 * list_bytes + range_susp_bytes(R) + range_floor_bytes(R);
-            ScoreArgs ca = a;
-            ca.cand = reinterpret_cast<uint64_t*>(cb);
-            ca.cand_cnt = reinterpret_cast<int32_t*>(cb + align_up((size_t)Bi * 4 * kCandCap * 8));
-            ca.cand_cap = kCandCap;
-            rc = launch_lds<false, kCandidates>(ca, p, stream, dtype);
-            if (rc) return rc;
-            int32_t* oi = out_idx + R.u0 * k;
-            float* ov = out_val ? out_val + R.u0 * k : nullptr;
-            if (k <= 64) score_topk_cand_select<1><<<(unsigned)Bi, 64, 0, stream>>>(ca, mask_value, apply_sigmoid, oi, ov);
-            else if (k <= 128) score_topk_cand_select<2><<<(unsigned)Bi, 64, 0, stream>>>(ca, mask_value, apply_sigmoid, oi, ov);
-            else score_topk_cand_select<4><<<(unsigned)Bi, 64, 0, stream>>>(ca, mask_value, apply_sigmoid, oi, ov);
-            LGX_LAUNCH_CHECK();
-            continue;
-        } else if (seeded_sweep(p, mm, n_items, dtype)) {
+        if (seeded_sweep(p, mm, n_items)) {
             rc = LGX_OK;
             for (int64_t lo = 0, hi = kSeedItems; lo < n_items && rc == LGX_OK; lo = hi, hi *= 2) {
                 ScoreArgs st = a;

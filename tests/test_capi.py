@@ -199,17 +199,16 @@ def test_strat_thresholds_reproduce_float16_labels(mn, mx, num_fold):
     assert np.array_equal(got, ref)
 
 
-def test_score_topk_plan_large_full_sweeps():
-    """Host only (lgx_score_topk_plan): from 262 144 items a bf16 full sweep runs as the candidate
-    sweep (score floors, every score above them into HBM, the exact per-user top-k after), an fp32
-    one in seeded stages; smaller catalogs and catalog-split launches run as one launch."""
+def test_score_topk_plan_seeds_large_full_sweeps():
+    """Host only (lgx_score_topk_plan): the full-sweep LDS plan is swept in seeded stages once the
+    catalog reaches 262 144 items; smaller catalogs and catalog-split launches run as one launch."""
     import torch
     from factors_of_serendipity_recommendation_amd import ops
     big = ops.score_topk_plan(1_000_000, 1_000_000, 256, torch.bfloat16, 20)
-    assert big.split("; ")[0].endswith("full-sweep (candidates above score floors) n_splits=1 utiles=3840"), big
-    assert "candidates" not in big.split("; ")[1] and "seeded" not in big
-    assert "candidates" in ops.score_topk_plan(65536, 262_144, 256, torch.bfloat16, 20)
-    assert "candidates" not in ops.score_topk_plan(65536, 262_143, 256, torch.bfloat16, 20)
-    assert "candidates" not in ops.score_topk_plan(4096, 1_000_000, 256, torch.bfloat16, 20)
+    assert big.split("; ")[0].endswith("full-sweep (seeded in stages) n_splits=1 utiles=3840"), big
+    assert "seeded" not in big.split("; ")[1]
+    assert "seeded" in ops.score_topk_plan(65536, 262_144, 256, torch.bfloat16, 20)
+    assert "seeded" not in ops.score_topk_plan(65536, 262_143, 256, torch.bfloat16, 20)
+    assert "seeded" not in ops.score_topk_plan(4096, 1_000_000, 256, torch.bfloat16, 20)
     f32 = ops.score_topk_plan(262_144, 1_000_000, 256, torch.float32, 20)
     assert f32.endswith("full-sweep (seeded in stages) n_splits=1 utiles=2048"), f32

@@ -95,11 +95,9 @@ def test_c5_scoring_full_sweep_plan_d256():
     catalog-split launch for the 67-tile remainder) at d=256 bf16 with the train mask."""
     B, I, d, k = 256 * (256 + 67), 100_000, 256, 20
     plan = ops.score_topk_plan(B, I, d, torch.bfloat16, k)
-    # the bench's 1M-item catalog runs its full sweep as the candidate sweep
-    # (test_candidate_full_sweep_equals_one_sweep), pinned at full size by
-    # test_c5_full_catalog_1m_items_bench_plan
-    bench = ops.score_topk_plan(1_000_000, 1_000_000, d, torch.bfloat16, k).replace(
-        " (candidates above score floors)", "")
+    # the bench's 1M-item catalog seeds its full sweep (test_seeded_full_sweep_equals_one_sweep)
+    # the bench's 1M-item catalog is pinned at full size by test_c5_full_catalog_1m_items_bench_plan
+    bench = ops.score_topk_plan(1_000_000, 1_000_000, d, torch.bfloat16, k).replace(" (seeded in stages)", "")
     kinds = [p.split(" users")[0] + " " + p.split(") ")[1].split(" n_splits")[0] for p in plan.split("; ")]
     bkinds = [p.split(" users")[0] + " " + p.split(") ")[1].split(" n_splits")[0] for p in bench.split("; ")]
     assert kinds == bkinds and "full-sweep" in plan and len(kinds) == 2, (plan, bench)
@@ -170,16 +168,14 @@ def test_full_sweep_masks_on_the_top_items(n_top, n_rand):
     assert torch.allclose(val[sel].double(), got, rtol=1e-5, atol=1e-5)
 
 
-def test_candidate_full_sweep_equals_one_sweep():
-    """bf16 catalogs of >= 262 144 items run the full sweep as the candidate sweep: score floors
-    over the first 16 384 items, every score at or above its floor into HBM, the exact top-k of the
-    unmasked candidates per user.  Masks put every user's own best first-16 K items (and random ones
-    everywhere) out of play.  The lists must equal, as sets with their values, the one-launch running
-    walk (the min/max variant takes neither floors nor candidates) and the float64 top-k of the
-    unmasked items."""
+def test_seeded_full_sweep_equals_one_sweep():
+    """Catalogs of >= 262 144 items run the full sweep in stages ([0, 16384), [16384, 32768), ...
+    doubling, then the rest), each seeding the next.  Masks put every user's own best first-stage items (and random
+    ones everywhere) out of play.  The lists must equal, as sets, the one-launch sweep
+    (the min/max variant never seeds) and the float64 top-k of the unmasked items."""
     B, I, d, k = 256 * 256, 300_000, 256, 20
     plan = ops.score_topk_plan(B, I, d, torch.bfloat16, k)
-    assert "full-sweep (candidates above score floors)" in plan, plan
+    assert "full-sweep (seeded in stages)" in plan, plan
     g = torch.Generator(device=DEV).manual_seed(29)
     Q = (torch.randn(B, d, device=DEV, generator=g) / 16).bfloat16()
     items = (torch.randn(I, d, device=DEV, generator=g) / 16).bfloat16()
@@ -209,38 +205,6 @@ def test_candidate_full_sweep_equals_one_sweep():
     assert (got >= kth - 1e-5 * kth.abs().clamp(min=1.0)).all()
 
 
-def test_candidate_regions_compact_under_ties():
-    """135,000 equal item rows after the floor window: a user whose score on that row reaches its
-    floor meets them all as candidates; its regions run full and compact in place (their k best keys
-    kept, the threshold raised to the k-th key, ties broken by the lower item id) -- several times
-    over the sweep -- while the other users never compact.  The lists equal, as sets with their
-    values, the one-launch running walk's."""
-    B, I, d, k = 256 * 256, 270_000, 64, 20
-    plan = ops.score_topk_plan(B, I, d, torch.bfloat16, k)
-    assert "candidates above score floors" in plan, plan
-    g = torch.Generator(device=DEV).manual_seed(71)
-    items = (torch.randn(I, d, device=DEV, generator=g) / 8).bfloat16()
-    items[100_000:235_000] = items[50_000]
-    Q = (torch.randn(B, d, device=DEV, generator=g) / 8).bfloat16()
-    # the users whose score on the repeated row is in their float64 top 40 of the first 16 K items
-    s_rep = (Q.double() @ items[50_000].double())
-    top40 = torch.cat([torch.topk(Q[u0:u0 + 8192].double() @ items[:16384].double().T, 40, dim=1).values[:, -1]
-                       for u0 in range(0, B, 8192)])
-    heavy = int((s_rep >= top40).sum())
-    assert 0 < heavy < B // 16, heavy
-    m = torch.randint(0, I, (B, 30), device=DEV, generator=g).sort(1).values
-    keep = torch.ones_like(m, dtype=torch.bool)
-    keep[:, 1:] = m[:, 1:] != m[:, :-1]
-    indptr = torch.zeros(B + 1, dtype=torch.int64, device=DEV)
-    indptr[1:] = torch.cumsum(keep.sum(1), 0)
-    mask = (indptr, m[keep].to(torch.int32))
-    idx, val = lgx.score_topk(Q, items, k, mask=mask)
-    idx1, val1, _ = lgx.score_topk(Q, items, k, mask=mask, want_minmax=True)
-    ka, kb = torch.sort(idx.long(), 1), torch.sort(idx1.long(), 1)
-    assert torch.equal(ka.values, kb.values), "candidate lists differ from the running walk"
-    assert torch.equal(val.gather(1, ka.indices), val1.gather(1, kb.indices))
-
-
 @pytest.mark.parametrize("mode,dtype", [("full-sweep", torch.bfloat16), ("split", torch.bfloat16),
                                         ("full-sweep", torch.float32), ("split", torch.float32)])
 def test_score_floors_with_ties_and_masked_group_maxima(mode, dtype):
@@ -259,8 +223,7 @@ def test_score_floors_with_ties_and_masked_group_maxima(mode, dtype):
         B, I = 18 * 256, 1_000_000
     plan = ops.score_topk_plan(B, I, d, dtype, k)
     if mode == "full-sweep":
-        want = "candidates above score floors" if dtype == torch.bfloat16 else "seeded in stages"
-        assert f"full-sweep ({want})" in plan, plan
+        assert "full-sweep (seeded in stages)" in plan, plan
     else:
         ns = int(re.search(r"n_splits=(\d+)", plan).group(1))
         assert "full-sweep" not in plan and "split" in plan and ns > 1, plan
@@ -301,11 +264,11 @@ def test_score_floors_with_ties_and_masked_group_maxima(mode, dtype):
 
 @pytest.mark.parametrize("d,k,rows", [(64, 1, False), (128, 7, True), (128, 32, False), (256, 20, True),
                                       (96, 20, True)])
-def test_candidate_sweep_shapes(d, k, rows):
-    """The candidate sweep across the bf16 LDS kernel's shapes (d, k) and with user_rows: lists equal,
-    as sets with their values, the one-launch running walk of the min/max variant."""
+def test_seeded_sweep_shapes(d, k, rows):
+    """The seeded stages across the LDS kernel's shapes (d, k) and with user_rows: lists equal, as
+    sets, the one-launch sweep of the unseeded min/max variant."""
     B, I = 256 * 256, 270_000
-    assert "candidates above score floors" in ops.score_topk_plan(B, I, d, torch.bfloat16, k)
+    assert "seeded in stages" in ops.score_topk_plan(B, I, d, torch.bfloat16, k)
     g = torch.Generator(device=DEV).manual_seed(31 + d + k)
     n_q = B + 1000 if rows else B
     Q = (torch.randn(n_q, d, device=DEV, generator=g) / 16).bfloat16()
@@ -393,14 +356,14 @@ def _masked_topk_check(Q, items, idx, val, mask, sel, k, chunk=250):
 def test_c5_full_catalog_1m_items_bench_plan():
     """BASELINE configs[4] at its own catalog: 82,688 users x 1,000,000 items, d=256 bf16, top-20,
     50 masked items per user.  The launch plan is the bench's (1 M users) launch for launch: the
-    candidate sweep (floors, candidates, exact fallback, per-user select) over whole rounds of user
-    tiles and the catalog-split tail with 3 splits -- the mode included in the comparison.  1,500
-    users of each launch are checked against float64 scores on the device."""
+    full sweep seeded in stages (7 launches over [0,16384), ..., [524288, 1M)) and the catalog-split
+    tail with 3 splits -- "seeded" included in the comparison.  1,500 users of each launch are
+    checked against float64 scores on the device."""
     B, I, d, k = 256 * (256 + 67), 1_000_000, 256, 20
     plan = ops.score_topk_plan(B, I, d, torch.bfloat16, k)
     bench = ops.score_topk_plan(1_000_000, I, d, torch.bfloat16, k)
     assert _plan_kinds(plan) == _plan_kinds(bench), (plan, bench)
-    assert "full-sweep (candidates above score floors)" in plan and len(_plan_kinds(plan)) == 2
+    assert "full-sweep (seeded in stages)" in plan and len(_plan_kinds(plan)) == 2
     g = torch.Generator(device=DEV).manual_seed(55)
     Q = (torch.randn(B, d, device=DEV, generator=g) / 16).bfloat16()
     items = (torch.randn(I, d, device=DEV, generator=g) / 16).bfloat16()
