@@ -8,16 +8,18 @@
 // (recommend.py:163-164, :375-377).  The reference materialises the [B, I] rating matrix; here it
 // never leaves the accumulators.
 //
-// MI355X design (one file, four kernel families):
+// MI355X design (one file, three kernel families):
 //   * score_topk_bf16_lds / score_topk_f32_lds -- the LDS-ring walk: a workgroup keeps its users'
 //     rows in VGPRs (the MFMA B operand) and streams 64-item tiles of the catalog (the A operand)
 //     through an LDS ring filled by LDS-DMA; v_mfma_f32_16x16x32_bf16 / 16x16x4_f32.  Its modes:
-//     the running top-k with the mask (kTopK), the global min / max (kMinMaxOnly), the per-user score
-//     floors (kFloorOnly) that start an unseeded sweep's lists;
-//   * score_walk_f32_lds -- the same walk's dense modes: fp32 getUsersRating scores and the
-//     stratification labels of recommend.py:375-381, bit for bit the same f32 sums;
-//   * score_topk_kernel -- a register-fragment walk for the shapes the LDS walk does not cover, and
-//     score_dense_lds / strat_label_lds for the bf16 dense scores and labels;
+//     the running top-k with the mask (kTopK), the global min / max (kMinMaxOnly) and the per-user
+//     score floors (kFloorOnly) that start an unseeded sweep's lists;
+//   * score_topk_kernel -- a register-fragment walk (v_mfma_f32_32x32x16_bf16 / 32x32x2_f32) for
+//     the shapes the LDS walk does not cover; score_dense_lds / score_dense_kernel (getUsersRating's
+//     dense scores) and strat_label_lds (recommend.py's stratification labels) on the same
+//     register-staged 32x32 walk, so fused labels are the labels of the dense scores bit for bit
+//     (the 16x16x4 LDS ring measured slower for these write-heavy modes at every d:
+//     profiles/r04_walk_lab.txt);
 //   * score_topk_finalize -- one wave per user merges split lists (register bitonic network), adds
 //     the masked tail when fewer than k unmasked items exist and applies the optional sigmoid.
 #include <algorithm>
@@ -696,60 +698,6 @@ constexpr int kMinMaxOnly = 1;
 // it, and a sweep that starts its lists with this threshold drops no item of the exact top-k (ties
 // at the floor included: a filling list takes scores >= floor).  A product mode.
 constexpr int kFloorOnly = 2;
-// The fp32 walk's dense modes (lgx_score_dense and lgx_strat_labels_fused in fp32, d a multiple of
-// 64): every score of the tile leaves the accumulators -- as an f32 score (kDenseScores, with the
-// reference's sigmoid under kDenseSigmoid, model.py:183) or as the stratification label of
-// recommend.py:375-381 with its per-user counts (kStratLabels).  One walk (items the A operand from
-// the LDS ring, users the B operand in registers, the same k order) gives both the same f32 sums,
-// so the fused labels equal the labels of the dense scores bit for bit.
-constexpr int kDenseScores = 3;
-constexpr int kDenseSigmoid = 4;
-constexpr int kStratLabels = 5;
-__host__ __device__ constexpr bool dense_mode(int m) { return m == kDenseScores || m == kDenseSigmoid || m == kStratLabels; }
-
-struct StratThr {
-    float t[32];
-    int n;
-    float base, inv;  // estimate: floor((s - base) * inv) is the label within +-1 (thresholds ~ evenly spaced)
-};
-
-// the label of score sc: the count of thresholds it reaches (recommend.py:379-381 restated on the f32
-// score, lgx_strat_thresholds).  T[j] = the score where label j starts (T[0] = -inf, T[n + 1] =
-// +inf), TP[j] = {T[j], T[j + 1]}.  EST1: the host proved the estimate within one of the label, so
-// one branch-free step each way corrects it; otherwise an exact walk from the estimate.
-template <bool EST1>
-__device__ __forceinline__ uint32_t strat_label_of(float sc, const StratThr& thr, const float* T, const float2* TP) {
-    const float x = (sc - thr.base) * thr.inv;
-    int l = (x >= (float)thr.n || x != x) ? thr.n : (x < 0.0f ? 0 : (int)x);  // NaN -> n, as label_of
-    if (EST1) {
-        const float2 tp = TP[l];  // T[l], T[l + 1]
-        return (uint32_t)(l - (sc < tp.x && l > 0 ? 1 : 0) + (sc >= tp.y && l < thr.n ? 1 : 0));
-    }
-    while (l > 0 && sc < T[l]) --l;
-    while (l < thr.n && sc >= T[l + 1]) ++l;
-    return (uint32_t)l;
-}
-
-// the reference's sigmoid (model.py:183) over dense score matrices: exp2 and reciprocal on the
-// transcendental unit, ~1e-6 relative to 1 / (1 + e^-x) (tests: 1e-5); the exact expf / IEEE division
-// form is ~20 VALU per score and made the bf16 [4096, 1M] getUsersRating VALU-bound (3.67 -> 5.37 ms).
-// Limits hold: x -> -inf gives rcp(inf) = 0, x -> +inf rcp(1) = 1.
-__device__ __forceinline__ float fast_sigmoid(float x) {
-    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.44269504088896341f));
-}
-
-// outputs of the dense modes
-struct WalkOut {
-    float* scores;   // kDenseScores / kDenseSigmoid: [B, n_items] f32
-    int8_t* labels;  // kStratLabels: [B, n_items] int8
-    int32_t* hist;   // kStratLabels: [B, thr.n + 1] label counts (added to), or nullptr
-    StratThr thr;
-    int vec4;        // n_items % 4 == 0 and 16-B aligned rows: one 16-B / 4-B store per 4 items
-    int est1;        // kStratLabels: the label estimate is within one of the label (host-proved)
-};
-// label counts of the workgroup's users in LDS, stride 17: the 16 users of a lane group sit in 16
-// different banks
-constexpr int kHistStride = 17;
 
 template <int KSTEPS, int WAVES = 8, int NACC = 2, int ESZ = 2>
 struct LdsGeom {
@@ -780,48 +728,17 @@ __device__ __forceinline__ void lds_dma16(const void* sbase, uint32_t voff, uint
 }
 #pragma clang diagnostic pop
 
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n; the counter has 6 bits, but the walks that issue
-// no stores inside the ring loop keep the 15-entry switch (conservative above 15: the larger jump
-// table costs the register-tight top-k bodies a spill)
-template <bool WIDE = false>
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (conservative above 15)
 __device__ __forceinline__ void wait_vmcnt_le(int n) {
 #define LGX_VMW(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-    if (!WIDE || n <= 15) {
-        switch (n) {
-            LGX_VMW(1) LGX_VMW(2) LGX_VMW(3) LGX_VMW(4) LGX_VMW(5) LGX_VMW(6) LGX_VMW(7) LGX_VMW(8) LGX_VMW(9) LGX_VMW(10) LGX_VMW(11) LGX_VMW(12) LGX_VMW(13) LGX_VMW(14) LGX_VMW(15)
-            default:
-                if (n >= 16) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-    } else {
-        switch (n) {
-            LGX_VMW(16) LGX_VMW(17) LGX_VMW(18) LGX_VMW(19) LGX_VMW(20) LGX_VMW(21) LGX_VMW(22) LGX_VMW(23)
-             LGX_VMW(24) LGX_VMW(25) LGX_VMW(26) LGX_VMW(27) LGX_VMW(28) LGX_VMW(29) LGX_VMW(30) LGX_VMW(31)
-             LGX_VMW(32) LGX_VMW(33) LGX_VMW(34) LGX_VMW(35) LGX_VMW(36) LGX_VMW(37) LGX_VMW(38) LGX_VMW(39)
-             LGX_VMW(40) LGX_VMW(41) LGX_VMW(42) LGX_VMW(43) LGX_VMW(44) LGX_VMW(45) LGX_VMW(46) LGX_VMW(47)
-             LGX_VMW(48) LGX_VMW(49) LGX_VMW(50) LGX_VMW(51) LGX_VMW(52) LGX_VMW(53) LGX_VMW(54) LGX_VMW(55)
-             LGX_VMW(56) LGX_VMW(57) LGX_VMW(58) LGX_VMW(59) LGX_VMW(60) LGX_VMW(61) LGX_VMW(62) LGX_VMW(63)
-            
-            default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
-        }
+    switch (n) {
+        LGX_VMW(1) LGX_VMW(2) LGX_VMW(3) LGX_VMW(4) LGX_VMW(5) LGX_VMW(6) LGX_VMW(7) LGX_VMW(8)
+        LGX_VMW(9) LGX_VMW(10) LGX_VMW(11) LGX_VMW(12) LGX_VMW(13) LGX_VMW(14) LGX_VMW(15)
+        default:
+            if (n >= 16) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 #undef LGX_VMW
-}
-
-// Global stores the LDS walk counts itself: one instruction each, never merged, dropped or
-// predicated away by the compiler.  vmcnt counts loads, stores and LDS-DMA together and retires them
-// in issue order, so every store issued after the refill a wait is for must be allowed for in that
-// wait, or the wait also waits for the newest refills; an epilogue reports the stores it issued
-// (a lane with nothing to store writes to g_store_sink instead, so the count stays wave-uniform).
-__device__ uint4 g_store_sink[4];
-__device__ __forceinline__ void st_u8(void* p, uint32_t v) {
-    asm volatile("global_store_byte %0, %1, off" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void st_u32(void* p, uint32_t v) {
-    asm volatile("global_store_dword %0, %1, off" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void st_u128(void* p, u32x4 v) {
-    asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
 }
 
 __device__ __forceinline__ uint32_t lds_u32(const void* p) {
@@ -859,10 +776,9 @@ constexpr int kBf16LdsWaves = 8;
 constexpr int kF32LdsWaves = 4;
 template <int DT, int KSTEPS, bool MINMAX, int MODE, int WAVES, int NACC, bool STAGGER>
 __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreArgs a, int xcd_affine,
-                                                    int64_t n_utiles, int nbuf, const WalkOut& o = WalkOut{}) {
+                                                    int64_t n_utiles, int nbuf) {
     constexpr bool F32 = DT == LGX_DTYPE_F32;
     static_assert(NACC == 2 && (F32 || KSTEPS % 2 == 0), "16x16 walk: 64-item tiles, bf16 d a multiple of 32");
-    static_assert(!dense_mode(MODE) || (F32 && !MINMAX), "dense modes: the fp32 walk");
     // SKIP: the fast-path test runs on the MFMA output layout itself (lane l holds 16 scores of user
     // l & 15 and 16 of user 16 + (l & 15)); the regroup into the top-k layout (16 v_permlane16_swap)
     // is paid only by tiles that have a survivor.  Min / max needs every score: not with MINMAX.
@@ -898,17 +814,6 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     const bool user_ok = b < a.B;
     uint4 uf[UFN];
     const int r16 = lane & 15, q4 = lane >> 4;
-    // kStratLabels: the per-user label counts and the thresholds, in LDS after the ring (published by
-    // the prologue's barrier)
-    uint32_t* hc = reinterpret_cast<uint32_t*>(smem + (size_t)nbuf * G::TILE);
-    float2* TP = reinterpret_cast<float2*>(hc + G::USERS * kHistStride);
-    float* T = reinterpret_cast<float*>(TP + 34);
-    if constexpr (MODE == kStratLabels) {
-        for (int e = threadIdx.x; e < G::USERS * kHistStride; e += WAVES * 64) hc[e] = 0u;
-        auto thr_at = [&](int j) { return j == 0 ? -INFINITY : (j <= o.thr.n ? o.thr.t[j - 1] : INFINITY); };
-        if (threadIdx.x < 34) T[threadIdx.x] = thr_at(threadIdx.x);
-        if (threadIdx.x < 33) TP[threadIdx.x] = make_float2(thr_at(threadIdx.x), thr_at(threadIdx.x + 1));
-    }
     // B fragment (ub, s) at uf[ub * NS + s]: user 16 ub + r16, 16-B chunk 4 s + q4 of its row
 #pragma unroll
     for (int ub = 0; ub < 2; ++ub) {
@@ -984,10 +889,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(ahead, ntiles) - 1));
     __syncthreads();
     int buf = 0, sbuf = ahead;  // buffer of tile t / of tile t + ahead
-    // staggered: the upper half of the waves runs each epilogue one tile late (below).  The unstaggered
-    // dense walk runs every epilogue late: its stores are then younger than the next refill and have
-    // a tile of MFMAs to drain before the next vmcnt wait, which would otherwise wait for them
-    const bool late = STAGGER ? MODE != kMinMaxOnly && wave >= WAVES / 2 : dense_mode(MODE);  // wave-uniform
+    const bool late = STAGGER && MODE != kMinMaxOnly && wave >= WAVES / 2;  // wave-uniform
     f32x16 acc0, acc1;  // late waves: tile t-1's scores, held across the barrier
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     f32x4 c[2][4];      // 16x16x32 accumulators: c[ub][ib] = items 16 ib + 4 (lane >> 4) + reg, user 16 ub + (lane & 15)
@@ -1117,109 +1019,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
                 gm[1][ib][r] = in ? fmaxf(gm[1][ib][r], c[1][ib][r]) : gm[1][ib][r];
             }
     };
-    // dense modes: lane (q4, r16) holds items e0 + 16 ib + 4 q4 + 0..3 of user 16 ub + r16
-    // counted stores of the current iteration / a drain (vmcnt(0)) taken by an epilogue
-    int vm_stores = 0;
-    bool vm_drained = false;
-    auto drain_stores = [&]() {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        vm_drained = true;
-        vm_stores = 0;
-    };
-    // whole tiles: 8 counted 16-B stores per wave (32 4-B stores when rows are not 16-B aligned),
-    // padding users' lanes into the sink; the split's partial last tile: plain stores, then a drain
-    auto dense_tile = [&](int64_t e0) {
-        const int64_t rem = i_end - e0;  // items of the tile inside the split
-        const bool whole = rem >= G::TILE_ITEMS;  // wave-uniform
-#pragma unroll
-        for (int ub = 0; ub < 2; ++ub) {
-            const int64_t bu = utile * G::USERS + wave * kUsersPerWave + 16 * ub + r16;
-            const bool uok = bu < a.B;
-            float* row = o.scores + (uok ? bu : 0) * a.n_items + e0;
-#pragma unroll
-            for (int ib = 0; ib < 4; ++ib) {
-                const int off = 16 * ib + 4 * q4;
-                float v[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = MODE == kDenseSigmoid ? fast_sigmoid(c[ub][ib][r]) : c[ub][ib][r];
-                if (whole && o.vec4) {
-                    st_u128(uok ? static_cast<void*>(row + off) : static_cast<void*>(g_store_sink),
-                            u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
-                                  __float_as_uint(v[3])});
-                } else if (whole) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        st_u32(uok ? static_cast<void*>(row + off + r) : static_cast<void*>(g_store_sink),
-                               __float_as_uint(v[r]));
-                } else if (uok) {
-                    if (o.vec4 && off + 4 <= rem) {
-                        *reinterpret_cast<float4*>(row + off) = make_float4(v[0], v[1], v[2], v[3]);
-                    } else {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r)
-                            if (off + r < rem) row[off + r] = v[r];
-                    }
-                }
-            }
-        }
-        if (whole) vm_stores += o.vec4 ? 8 : 32;
-        else drain_stores();
-    };
-    // labels: the same store accounting as dense_tile (8 counted 4-B stores per whole tile, 32 1-B
-    // stores when rows are not 4-B aligned)
-    auto label_tile = [&](auto est_tag, int64_t e0) {
-        constexpr bool EST1 = decltype(est_tag)::value;
-        const int64_t rem = i_end - e0;
-        const bool whole = rem >= G::TILE_ITEMS;  // wave-uniform
-#pragma unroll
-        for (int ub = 0; ub < 2; ++ub) {
-            const int64_t bu = utile * G::USERS + wave * kUsersPerWave + 16 * ub + r16;
-            const bool uok = bu < a.B;
-            int8_t* row = o.labels + (uok ? bu : 0) * a.n_items + e0;
-            uint32_t* hu = hc + (wave * kUsersPerWave + 16 * ub + r16) * kHistStride;
-#pragma unroll
-            for (int ib = 0; ib < 4; ++ib) {
-                const int off = 16 * ib + 4 * q4;
-                uint32_t l[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) l[r] = strat_label_of<EST1>(c[ub][ib][r], o.thr, T, TP);
-                if (o.hist && uok) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        if (off + r < rem) atomicAdd(hu + l[r], 1u);
-                }
-                const uint32_t w = l[0] | (l[1] << 8) | (l[2] << 16) | (l[3] << 24);
-                if (whole && o.vec4) {
-                    st_u32(uok ? static_cast<void*>(row + off) : static_cast<void*>(g_store_sink), w);
-                } else if (whole) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        st_u8(uok ? static_cast<void*>(row + off + r) : static_cast<void*>(g_store_sink),
-                              (w >> (8 * r)) & 255);
-                } else if (uok) {
-                    if (o.vec4 && off + 4 <= rem) {
-                        *reinterpret_cast<uint32_t*>(row + off) = w;
-                    } else {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r)
-                            if (off + r < rem) row[off + r] = (int8_t)((w >> (8 * r)) & 255);
-                    }
-                }
-            }
-        }
-        if (whole) vm_stores += o.vec4 ? 8 : 32;
-        else drain_stores();
-    };
     auto epilogue = [&](int64_t e0) {
-        if constexpr (MODE == kDenseScores || MODE == kDenseSigmoid) {
-            dense_tile(e0);
-            return;
-        }
-        if constexpr (MODE == kStratLabels) {
-            if (o.est1) label_tile(std::true_type{}, e0);
-            else label_tile(std::false_type{}, e0);
-            return;
-        }
         if constexpr (MODE == kMinMaxOnly) {
             minmax_tile();
             return;
@@ -1285,44 +1085,20 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         // candidates, and skip the two cross-lane reads
         if (SKIP && __ballot(st.tau != tau_before) != 0ull) refresh_taus();
     };
-    // counted stores of iterations t-2, t-1, t (the refill of tile t+1 was issued at the start of
-    // iteration t+1-ahead, ahead <= 3: every store of those iterations is younger than it)
-    int vs0 = 0, vs1 = 0;
     for (int64_t t = 0; t < ntiles; ++t) {
         const int64_t t0 = tile_start(t);
-        vm_stores = 0;
-        vm_drained = false;
         if (t + ahead < ntiles) stage(sbuf, tile_start(t + ahead));
         if (late && t > 0) epilogue(prev_t0);
         compute();
         if (!late) epilogue(t0);
         prev_t0 = t0;
-        if (vm_drained) vs0 = vs1 = 0;  // a drain retired everything issued before it
-        const int younger = vm_stores + (ahead >= 2 ? vs1 : 0) + (ahead >= 3 ? vs0 : 0);
-        vs0 = vs1;
-        vs1 = vm_stores;
-        // tiles t+2 .. t+ahead and the stores issued since tile t+1's refill may stay in flight;
-        // tile t+1 must have landed
-        wait_vmcnt_le<dense_mode(MODE)>(
-            my_pieces * (int)max<int64_t>(0, min<int64_t>(t + ahead, ntiles - 1) - (t + 1)) + younger);
+        // tiles t+2 .. t+ahead may stay in flight; tile t+1 must have landed
+        wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(t + ahead, ntiles - 1) - (t + 1)));
         __syncthreads();
         buf = buf + 1 == nbuf ? 0 : buf + 1;
         sbuf = sbuf + 1 == nbuf ? 0 : sbuf + 1;
     }
     if (late && ntiles > 0) epilogue(prev_t0);
-    if constexpr (MODE == kStratLabels) {  // the workgroup's counts into the global histogram
-        __syncthreads();
-        if (o.hist) {
-            const int64_t u0 = utile * G::USERS;
-            for (int e = threadIdx.x; e < G::USERS * kHistStride; e += WAVES * 64) {
-                const int uu = e / kHistStride, l = e % kHistStride;
-                const uint32_t cnt = hc[e];
-                if (cnt && l <= o.thr.n && u0 + uu < a.B) atomicAdd(o.hist + (u0 + uu) * (o.thr.n + 1) + l, (int32_t)cnt);
-            }
-        }
-        return;
-    }
-    if constexpr (MODE == kDenseScores || MODE == kDenseSigmoid) return;
     if constexpr (MODE == kMinMaxOnly) {
 #pragma unroll
         for (int m = 32; m > 0; m >>= 1) {
@@ -1404,38 +1180,29 @@ void score_topk_f32_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf)
         smem, a, xcd_affine, n_utiles, nbuf);
 }
 
-// the fp32 walk's dense modes (lgx_score_dense / lgx_strat_labels_fused in fp32, d = 4 KS).  d <= 128:
-// 8 waves x 32 users, two per SIMD, staggered as the bf16 top-k walk is -- one wave's epilogue (labels
-// and their counts, or the score stores) runs beside its partner's MFMAs.  With one wave per SIMD (the
-// f32 top-k shape) the d=64 labels took 10.6 ms per 4096 x 1M batch: nothing issued MFMAs during an
-// epilogue.  d >= 192: the 32 users' rows take 96-128 VGPRs, two waves per SIMD spill (d=256: 72 B of
-// scratch), and a tile is 12-16 K MFMA cycles per wave against a ~1 K-cycle epilogue: 4 waves, one per
-// SIMD, every epilogue after the barrier.
-// (held to 128 VGPRs for two workgroups per CU, the d = 64 walk spills 112-140 B: one per CU)
-__host__ __device__ constexpr int walk_waves(int ks) { return ks <= 8 ? 8 : 4; }
-template <int KSTEPS, int MODE>
-__global__ __launch_bounds__(walk_waves(KSTEPS) * 64)
-__attribute__((amdgpu_waves_per_eu(walk_waves(KSTEPS) / 4, walk_waves(KSTEPS) / 4)))
-void score_walk_f32_lds(ScoreArgs a, WalkOut o, int xcd_affine, int64_t n_utiles, int nbuf) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    score_topk_lds_body<LGX_DTYPE_F32, KSTEPS, false, MODE, walk_waves(KSTEPS), 2, walk_waves(KSTEPS) == 8>(
-        smem, a, xcd_affine, n_utiles, nbuf, o);
-}
-
 __global__ void minmax_finish(const uint32_t* mm, float* out) {
     out[0] = unord_f32(mm[0]);
     out[1] = unord_f32(mm[1]);
 }
 
 // one wave per query: merge the split lists, masked tail, optional sigmoid (k <= 64 R)
-// the merged list of user b -> out_idx / out_val (k <= 64 R): keys in order, then -- when fewer than k
-// unmasked items exist -- the user's masked items with mask_value (Procedure.py:134 ranks them below
-// every real score); the optional sigmoid on the scores (model.py:183)
 template <int R>
-__device__ __forceinline__ void emit_topk(const WaveList<R>& top, const ScoreArgs& a, int64_t b, int lane,
-                                          float mask_value, int apply_sigmoid, int32_t* __restrict__ out_idx,
-                                          float* __restrict__ out_val) {
+__global__ __launch_bounds__(64) void score_topk_finalize(ScoreArgs a, float mask_value, int apply_sigmoid,
+                                                          int32_t* __restrict__ out_idx, float* __restrict__ out_val,
+                                                          float* __restrict__ minmax_out) {
+    const int lane = threadIdx.x;
+    const int64_t b = blockIdx.x;
     const int k = a.k;
+    const int64_t total = (int64_t)a.n_splits * k;
+    const float* ps = a.part_score + (size_t)b * total;
+    const int32_t* pi = a.part_idx + (size_t)b * total;
+    WaveList<R> top;
+    top.clear();
+    for (int64_t base = 0; base < total; base += 64) {
+        const int64_t j = base + lane;
+        const uint64_t cand = (j < total && pi[j] >= 0) ? make_key(ps[j], pi[j]) : 0ull;
+        top.push(cand, k, lane);
+    }
     int n_real = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) n_real += __popcll(__ballot(top.t[r] != 0ull));
@@ -1458,33 +1225,6 @@ __device__ __forceinline__ void emit_topk(const WaveList<R>& top, const ScoreArg
         out_idx[b * k + e] = idx;
         if (out_val) out_val[b * k + e] = val;
     }
-}
-
-// user b's split lists (the LDS walk's flush) merged into one top-k
-template <int R>
-__device__ __forceinline__ void merge_parts(WaveList<R>& top, const ScoreArgs& a, int64_t b, int lane) {
-    const int k = a.k;
-    const int64_t total = (int64_t)a.n_splits * k;
-    const float* ps = a.part_score + (size_t)b * total;
-    const int32_t* pi = a.part_idx + (size_t)b * total;
-    for (int64_t base = 0; base < total; base += 64) {
-        const int64_t j = base + lane;
-        const uint64_t cand = (j < total && pi[j] >= 0) ? make_key(ps[j], pi[j]) : 0ull;
-        top.push(cand, k, lane);
-    }
-}
-
-// one wave per query: merge the split lists, masked tail, optional sigmoid (k <= 64 R)
-template <int R>
-__global__ __launch_bounds__(64) void score_topk_finalize(ScoreArgs a, float mask_value, int apply_sigmoid,
-                                                          int32_t* __restrict__ out_idx, float* __restrict__ out_val,
-                                                          float* __restrict__ minmax_out) {
-    const int lane = threadIdx.x;
-    const int64_t b = blockIdx.x;
-    WaveList<R> top;
-    top.clear();
-    merge_parts(top, a, b, lane);
-    emit_topk(top, a, b, lane, mask_value, apply_sigmoid, out_idx, out_val);
     if (minmax_out && b == 0 && lane == 0) {
         minmax_out[0] = unord_f32(a.minmax[0]);
         minmax_out[1] = unord_f32(a.minmax[1]);
@@ -1505,6 +1245,14 @@ __global__ void minmax_init(uint32_t* mm) {
 // scores written, not 64 GB.  Workgroup -> (user group, split) is XCD-aware: the workgroups of one
 // XCD (blockIdx mod 8) take splits s = xcd (mod 8), all user groups of a split back to back, so the
 // groups sharing a split also share that XCD's L2.
+// the reference's sigmoid (model.py:183) over dense score matrices: exp2 and reciprocal on the
+// transcendental unit, ~1e-6 relative to 1 / (1 + e^-x) (tests: 1e-5); the exact expf / IEEE division
+// form is ~20 VALU per score and made the bf16 [4096, 1M] getUsersRating VALU-bound (3.67 -> 5.37 ms).
+// Limits hold: x -> -inf gives rcp(inf) = 0, x -> +inf rcp(1) = 1.
+__device__ __forceinline__ float fast_sigmoid(float x) {
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.44269504088896341f));
+}
+
 constexpr int kDenseWaves = 8;
 constexpr int kDenseUsers = kDenseWaves * kUsersPerWave;
 
@@ -1683,6 +1431,11 @@ int kch_for(int dtype, int64_t d) {
 // (col, h) ends a tile holding 16 scores of ONE user (user u0 + col, items tile_row(r, h)): the
 // labels of items 8q + 4h + 0..3 pack into one dword store.  A label is the count of thresholds the
 // score reaches (lgx_strat_thresholds); nothing but the int8 labels leaves the chip.
+struct StratThr {
+    float t[32];
+    int n;
+    float base, inv;  // estimate: floor((s - base) * inv) is the label within +-1 (thresholds ~ evenly spaced)
+};
 
 // the label estimate of the kernel, on the host (same f32 operations, no contraction)
 inline int strat_estimate(float sc, const StratThr& thr) {
@@ -1727,7 +1480,9 @@ inline bool strat_estimate_within_one(const StratThr& thr) {
     }
 }
 
-// (strat_label_lds keeps the label counts of its 256 users in LDS the same way, kHistStride)
+// label counts of the workgroup's 256 users kept in LDS (stride 17: the 32 users of a wave sit in
+// 32 different banks), added to the global histogram once per workgroup
+constexpr int kHistStride = 17;
 
 template <int DT, int KCH, bool VEC4, bool EST1>
 __global__ __launch_bounds__(kDenseWaves * 64) void strat_label_lds(const void* Q, const int64_t* user_rows,
@@ -1753,7 +1508,9 @@ __global__ __launch_bounds__(kDenseWaves * 64) void strat_label_lds(const void* 
     const int h = lane >> 5, col = lane & 31;
     auto thr_at = [&](int j) { return j == 0 ? -INFINITY : (j <= thr.n ? thr.t[j - 1] : INFINITY); };
     if (threadIdx.x < 34) T[threadIdx.x] = thr_at(threadIdx.x);
-    if (threadIdx.x < 33) TP[threadIdx.x] = make_float2(thr_at(threadIdx.x), thr_at(threadIdx.x + 1));
+    // TP[n].y = NaN: the estimate path's upper compare is false at the last label without a guard
+    if (threadIdx.x < 33)
+        TP[threadIdx.x] = make_float2(thr_at(threadIdx.x), (int)threadIdx.x < thr.n ? thr_at(threadIdx.x + 1) : NAN);
     if (hist)
         for (int e = threadIdx.x; e < kDenseUsers * kHistStride; e += kDenseWaves * 64) hc[e] = 0u;
     const int64_t L = blockIdx.x, kk = L >> 3;
@@ -1792,7 +1549,20 @@ __global__ __launch_bounds__(kDenseWaves * 64) void strat_label_lds(const void* 
             *reinterpret_cast<uint4*>(&img[buf][r * RB + ((q ^ (r & 15)) * 16)]) = nx[j];
         }
     };
-    auto label = [&](float sc) { return strat_label_of<EST1>(sc, thr, T, TP); };
+    auto label = [&](float sc) {
+        const float x = (sc - thr.base) * thr.inv;
+        int l = (int)__builtin_amdgcn_fmed3f(x, 0.0f, (float)thr.n);  // clamp to [0, n], then truncate
+        if (x != x) l = thr.n;                                       // NaN -> n, as label_of
+        if (EST1) {
+            // the host proved |estimate - label| <= 1: one branch-free step each way.  TP[l] = {T[l],
+            // T[l + 1]} with TP[0].x = -inf and TP[n].y = NaN, so neither compare needs a range guard
+            const float2 tp = TP[l];
+            return (uint32_t)(l - (sc < tp.x ? 1 : 0) + (sc >= tp.y ? 1 : 0));
+        }
+        while (l > 0 && sc < T[l]) --l;  // exact whatever the estimate
+        while (l < thr.n && sc >= T[l + 1]) ++l;
+        return (uint32_t)l;
+    };
     if (i_begin >= i_end) return;  // workgroup-uniform
     load_tile(i_begin);
     store_tile(0);
@@ -1969,7 +1739,6 @@ inline int lds_ring_buffers(size_t tile, size_t lists, int wg_per_cu) {
 template <int KS, bool MM, int MODE>
 int launch_bf16_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     typedef LdsGeom<KS, kBf16LdsWaves, 2> G;
-    // the candidate sweep keeps no lists in LDS: the ring takes it (4 tiles at d = 256)
     const size_t lists = (size_t)kBf16LdsWaves * list_bytes_per_wave(a.k, kPendBf16Lds);
     const int nbuf = lds_ring_buffers(G::TILE, lists, 1);
     const size_t shmem = (size_t)nbuf * G::TILE + lists;
@@ -2004,15 +1773,23 @@ int launch_f32_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t st
 template <bool MM, int MODE = kTopK>
 int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream, int dtype = LGX_DTYPE_BF16) {
     const int ksteps = (int)(a.d / 16);
-    if (dtype == LGX_DTYPE_F32) {
-        switch (ksteps) {
-            case 4: return launch_f32_lds_kernel<4, MM, MODE>(a, p, stream);
-            case 8: return launch_f32_lds_kernel<8, MM, MODE>(a, p, stream);
-            case 12: return launch_f32_lds_kernel<12, MM, MODE>(a, p, stream);
-            case 16: return launch_f32_lds_kernel<16, MM, MODE>(a, p, stream);
-            default:
-                set_error("lgx_score_topk: no f32 LDS kernel for d=%lld", (long long)a.d);
-                return LGX_ERR_UNSUPPORTED;
+    if constexpr (MODE == kFloorOnly) {
+        if (dtype == LGX_DTYPE_F32) {
+            set_error("lgx_score_topk: score floors are a bf16 LDS kernel mode");
+            return LGX_ERR_UNSUPPORTED;
+        }
+    }
+    if constexpr (MODE != kFloorOnly) {
+        if (dtype == LGX_DTYPE_F32) {
+            switch (ksteps) {
+                case 4: return launch_f32_lds_kernel<4, MM, MODE>(a, p, stream);
+                case 8: return launch_f32_lds_kernel<8, MM, MODE>(a, p, stream);
+                case 12: return launch_f32_lds_kernel<12, MM, MODE>(a, p, stream);
+                case 16: return launch_f32_lds_kernel<16, MM, MODE>(a, p, stream);
+                default:
+                    set_error("lgx_score_topk: no f32 LDS kernel for d=%lld", (long long)a.d);
+                    return LGX_ERR_UNSUPPORTED;
+            }
         }
     }
 #define LGX_SL(KS) return launch_bf16_lds_kernel<KS, MM, MODE>(a, p, stream)
@@ -2030,54 +1807,6 @@ int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream, int d
             return LGX_ERR_UNSUPPORTED;
     }
 #undef LGX_SL
-}
-
-// The fp32 walk's dense modes (score_walk_f32_lds): d a multiple of 64 up to 256.  lgx_score_dense
-// and lgx_strat_labels_fused route fp32 through it by the same rule, so the fused labels are the
-// labels of lgx_score_dense's scores bit for bit at every d.
-inline bool f32_walk_eligible(int dtype, int64_t d) { return dtype == LGX_DTYPE_F32 && d % 64 == 0 && d >= 64 && d <= 256; }
-
-template <int KS, int MODE>
-int launch_f32_walk_ks(const ScoreArgs& a, const WalkOut& o, int xcd_affine, int64_t n_ut, hipStream_t stream) {
-    typedef LdsGeom<KS, walk_waves(KS), 2, 4> G;
-    const size_t extra = MODE == kStratLabels ? (size_t)G::USERS * kHistStride * 4 + 34 * 8 + 34 * 4 : 0;
-    const int nbuf = lds_ring_buffers(G::TILE, extra, 1);
-    const size_t shmem = (size_t)nbuf * G::TILE + extra;
-    int rc = set_lds_limit(score_walk_f32_lds<KS, MODE>, shmem);
-    if (rc) return rc;
-    score_walk_f32_lds<KS, MODE><<<(unsigned)(n_ut * a.n_splits), walk_waves(KS) * 64, shmem, stream>>>(
-        a, o, xcd_affine, n_ut, nbuf);
-    LGX_LAUNCH_CHECK();
-    return LGX_OK;
-}
-
-// one launch over every (user tile, catalog split): splits (a multiple of 8 when more than one, so
-// the workgroups of an XCD share a split's tiles in its L2) until >= 2 rounds of the 256 resident
-// workgroups, each split >= 8 tiles; no list-filling phase to repeat, so splitting costs nothing
-template <int MODE>
-int launch_f32_walk(const void* Q, const int64_t* user_rows, const void* items, int64_t B, int64_t n_items, int64_t d,
-                    const WalkOut& o, hipStream_t stream) {
-    const int64_t n_ut = ceil_div(B, (int64_t)walk_waves((int)(d / 16)) * kUsersPerWave);
-    const int64_t tiles = ceil_div(n_items, (int64_t)kTileItems);
-    int64_t s = 1;
-    if (n_ut < 2 * lds_resident()) {
-        s = std::min(ceil_div((int64_t)2 * lds_resident(), n_ut), std::max<int64_t>(1, tiles / 8));
-        if (s > 8) s = 8 * (s / 8);
-    }
-    const int64_t per = ceil_div(tiles, s) * kTileItems;
-    const int n = (int)ceil_div(n_items, per);
-    LGX_REQUIRE(n_ut * n < (1LL << 31), LGX_ERR_UNSUPPORTED, "score walk: %lld users is too many", (long long)B);
-    ScoreArgs a{Q, user_rows, items, B, n_items, d, nullptr, nullptr, 1, n, per, nullptr, nullptr, nullptr, nullptr};
-    const int affine = n % 8 == 0 ? 1 : 0;
-    switch (d / 16) {
-        case 4: return launch_f32_walk_ks<4, MODE>(a, o, affine, n_ut, stream);
-        case 8: return launch_f32_walk_ks<8, MODE>(a, o, affine, n_ut, stream);
-        case 12: return launch_f32_walk_ks<12, MODE>(a, o, affine, n_ut, stream);
-        case 16: return launch_f32_walk_ks<16, MODE>(a, o, affine, n_ut, stream);
-        default:
-            set_error("score walk: no f32 walk for d=%lld", (long long)d);
-            return LGX_ERR_UNSUPPORTED;
-    }
 }
 
 // A batch runs as up to two launches over user ranges.  In the LDS kernel's full-sweep mode every
@@ -2185,9 +1914,9 @@ extern "C" int lgx_score_topk_plan(int64_t B, int64_t n_items, int64_t d, int dt
                                  : (v1_waves(k) == 4 ? "score_topk_kernel<4 waves>" : "score_topk_kernel<1 wave>");
         const char* mode = p.lds ? (p.n_splits == 1 ? "full-sweep" : (p.xcd_affine ? "split-xcd" : "split"))
                                  : "split";
-        const char* how = seeded_sweep(p, false, n_items) ? " (seeded in stages)" : "";
         off += snprintf(buf + off, len - off, "%s%s users[%lld,%lld) %s%s n_splits=%d utiles=%lld",
-                        i ? "; " : "", kern, (long long)r[i].u0, (long long)r[i].u1, mode, how, p.n_splits,
+                        i ? "; " : "", kern, (long long)r[i].u0, (long long)r[i].u1, mode,
+                        seeded_sweep(p, false, n_items) ? " (seeded in stages)" : "", p.n_splits,
                         (long long)p.n_utiles);
     }
     return LGX_OK;
@@ -2332,14 +2061,6 @@ extern "C" int lgx_score_dense(const void* Q, const int64_t* user_rows, const vo
     LGX_REQUIRE(d > 0 && d % vec == 0 && kch > 0, LGX_ERR_UNSUPPORTED,
                 "lgx_score_dense: d=%lld must be a multiple of %lld and <= 256", (long long)d, (long long)vec);
     if (B == 0 || n_items == 0) return LGX_OK;
-    if (f32_walk_eligible(dtype, d)) {  // fp32: the 16x16x4 LDS-ring walk
-        LGX_REQUIRE(n_items < INT32_MAX, LGX_ERR_UNSUPPORTED, "lgx_score_dense: %lld items", (long long)n_items);
-        WalkOut o{};
-        o.scores = scores;
-        o.vec4 = n_items % 4 == 0 && ((uintptr_t)scores & 15) == 0;
-        return apply_sigmoid ? launch_f32_walk<kDenseSigmoid>(Q, user_rows, items, B, n_items, d, o, stream)
-                             : launch_f32_walk<kDenseScores>(Q, user_rows, items, B, n_items, d, o, stream);
-    }
     // splits: a multiple of 8 (one residue class per XCD), enough workgroups to fill the chip
     const int64_t n_ug = ceil_div(B, (int64_t)kDenseUsers);
     const int64_t tiles = ceil_div(n_items, 32);
@@ -2407,29 +2128,17 @@ extern "C" int lgx_strat_labels_fused(const void* Q, const int64_t* user_rows, c
     thr.inv = num_fold > 1 && std::isfinite(thr.t[num_fold - 1]) && thr.t[num_fold - 1] > thr.t[0]
                   ? (float)(num_fold - 1) / (thr.t[num_fold - 1] - thr.t[0]) : 1.0f / inter16;
     if (B == 0 || n_items == 0) return LGX_OK;
-    const bool vec4 = n_items % 4 == 0 && ((uintptr_t)labels & 3) == 0;
-    const bool est1 = strat_estimate_within_one(thr);
-    // counts in the scoring kernel (num_fold + 1 <= 17 bins), else a counting pass over the labels
-    const bool fuse_hist = num_fold + 1 <= kHistStride;
-    if (fuse_hist) LGX_HIP_CHECK(hipMemsetAsync(hist, 0, (size_t)B * (num_fold + 1) * sizeof(int32_t), stream));
-    if (f32_walk_eligible(dtype, d)) {  // fp32: the walk of lgx_score_dense's fp32 scores
-        WalkOut o{};
-        o.labels = labels;
-        o.hist = fuse_hist ? hist : nullptr;
-        o.thr = thr;
-        o.vec4 = vec4 ? 1 : 0;
-        o.est1 = est1 ? 1 : 0;
-        int rc = launch_f32_walk<kStratLabels>(Q, user_rows, items, B, n_items, d, o, stream);
-        if (rc) return rc;
-        if (fuse_hist) return lgx_strat_mask(labels, B, n_items, num_fold, mask_indptr, mask_indices, hist, stream_);
-        return lgx_strat_hist(labels, B, n_items, num_fold, mask_indptr, mask_indices, hist, stream_);
-    }
     const int64_t n_ug = ceil_div(B, (int64_t)kDenseUsers);
     const int64_t tiles = ceil_div(n_items, 32);
     const int64_t n_splits = std::max<int64_t>(8, std::min(8 * ceil_div(ceil_div(2048, n_ug), 8), 8 * ceil_div(tiles, 8)));
     const int64_t split_items = 32 * ceil_div(tiles, n_splits);
     const int64_t grid = n_ug * n_splits;
     LGX_REQUIRE(grid < (1LL << 31), LGX_ERR_UNSUPPORTED, "lgx_strat_labels_fused: %lld users is too many", (long long)B);
+    const bool vec4 = n_items % 4 == 0 && ((uintptr_t)labels & 3) == 0;
+    const bool est1 = strat_estimate_within_one(thr);
+    // counts in the scoring kernel (num_fold + 1 <= 17 bins), else a counting pass over the labels
+    const bool fuse_hist = num_fold + 1 <= kHistStride;
+    if (fuse_hist) LGX_HIP_CHECK(hipMemsetAsync(hist, 0, (size_t)B * (num_fold + 1) * sizeof(int32_t), stream));
 #define LGX_SL3(DTV, KC, V4)                                                                                      \
     if (est1)                                                                                                     \
         strat_label_lds<DTV, KC, V4, true><<<(unsigned)grid, kDenseWaves * 64, 0, stream>>>(                      \

@@ -425,12 +425,10 @@ def test_score_dense_lds_image(dtype, d):
 
 @pytest.mark.parametrize("B,I,d,sig,rows", [(100, 20_011, 256, True, False), (700, 3001, 192, False, True),
                                             (66_000, 301, 64, True, False), (4100, 12_345, 128, False, False)])
-def test_score_dense_f32_walk(B, I, d, sig, rows):
-    """fp32 getUsersRating (model.py:179-184) on the 16x16x4 LDS-ring walk (score_walk_f32_lds, d a
-    multiple of 64): split catalogs (B=100: one user tile, ~500 splits; 4100 users: 33 tiles x 16
-    XCD-affine splits), a full sweep per workgroup (66,000 users = 516 user tiles), catalogs that are
-    not a multiple of the 64-item tile or of 4 (scalar tail stores), user_rows, the sigmoid; against
-    float64 at the fp32 tolerance."""
+def test_score_dense_f32_shapes(B, I, d, sig, rows):
+    """fp32 getUsersRating (model.py:179-184) through score_dense_lds: the reference's 100-user
+    batch, 700 and 4100 users, 66,000 users over a 301-item catalog, catalogs that are not a multiple
+    of the 32-item tile or of 4, user_rows, the sigmoid; against float64 at the fp32 tolerance."""
     g = torch.Generator(device=DEV).manual_seed(B + d)
     n_q = B + 37 if rows else B
     Q = torch.randn(n_q, d, device=DEV, generator=g) / np.sqrt(d)

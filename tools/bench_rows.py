@@ -396,7 +396,7 @@ def row_f4(rows, reps):
     def sel():
         _lib.check(L.lgx_strat_select(labels.data_ptr(), B, I, hist.data_ptr(), F + 1, tgt.data_ptr(), 77,
                                       out.data_ptr(), Kc, cnt.data_ptr(), st), "lgx_strat_select")
-    def fused20():  # > 16 folds: the labels alone in the walk, the counts by a separate pass
+    def fused20():  # > 16 folds: the labels alone in the MFMA epilogue, the counts by a separate pass
         _lib.check(L.lgx_strat_labels_fused(eu.data_ptr(), None, ei.data_ptr(), B, I, d, _lib.LGX_DTYPE_F32, min16,
                                             inter16, 20, mp.data_ptr(), mi.data_ptr(), labels.data_ptr(),
                                             hist20.data_ptr(), st), "lgx_strat_labels_fused")
@@ -417,7 +417,7 @@ def row_f4(rows, reps):
          n * I, s, f"{n} users x {I} items: numpy dot + float16 labels + histograms (labels only)", 1,
          f"per batch: fused labels + counts {ms_f:.2f} ms (the counting pass over the labels it replaces: "
          f"{ms_h:.2f} ms), select "
-         f"{ms_p:.2f} ms; 20 folds (labels in the walk, counts by a separate pass) {ms_f20:.2f} ms; "
+         f"{ms_p:.2f} ms; 20 folds (labels in the MFMA epilogue, counts by a separate pass) {ms_f20:.2f} ms; "
          f"the two-step path: score_dense {ms_s:.2f} + labels {ms_l:.2f} ms; roofline: the "
          "fused kernel's f32 MFMA flops over the whole batch time")
     del S, labels

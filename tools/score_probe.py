@@ -1,6 +1,6 @@
 """Development: the bench's bf16 scoring leg shape (B users x 1M items, d=256, top-20, 50 masked
 items per user) timed with HIP events; run under rocprofv3 --kernel-trace --stats for the per-kernel
-split (floor pass, candidate sweep, exact fallback, per-user select).
+split (floor pass, the seeded stages, the split tail, the finalize).
 
   python tools/score_probe.py [B] [dtype]
 """
