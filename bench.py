@@ -307,12 +307,16 @@ def bench_propagation(args, rank, world, A, cfg, dtype, steps, warmup):
         # pull / reduce / epilogue are kernels, allgather_wait / exchange_wait the time the stream
         # sat behind a collective (the communication the schedule left exposed)
         ph = step.prop.phase_summary()
-        names = ["push", "allgather_wait", "pull", "exchange_wait", "reduce", "epilogue", "comm_exposed_ms"]
+        names = ["push", "allgather_wait", "pull", "exchange_wait", "exchange_sync", "reduce", "epilogue",
+                 "comm_exposed_ms"]
         mx = {n: max_over_ranks(float(ph.get(n, 0.0)), world) for n in names}
         out["comm_exposed_ms"] = mx.pop("comm_exposed_ms")
         out["phases_ms"] = mx
+        sync = ("; gloo has no device all-to-all: each exchange is a host-synchronous all-gather of the "
+                "slabs (exchange_sync), so this line is a rehearsal of the schedule, not of RCCL's overlap"
+                if not step.prop._a2a_native else "")
         out["phases_note"] = (f"ms per step on the compute stream, max over {world} ranks; push in "
-                              f"{len(step.prop.push_chunks)} chunks, each exchanged by its own all-to-all")
+                              f"{len(step.prop.push_chunks)} chunks, each exchanged by its own all-to-all{sync}")
     return out
 
 

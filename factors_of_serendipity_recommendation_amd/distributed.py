@@ -33,7 +33,9 @@ full tables).
 
 Diagnostics.  With record_phases set, every step stamps the compute stream after each phase
 (push, allgather_wait, pull, exchange_wait, reduce, epilogue); the waits are the time the stream
-sat behind a collective, i.e. the communication the schedule left exposed (phase_summary()).
+sat behind a collective, i.e. the communication the schedule left exposed (phase_summary()).  Under
+gloo (CPU tests, one-GPU rehearsals) the exchange is a host-synchronous all-gather: its time is
+stamped as exchange_sync, and counts as exposed.
 
 The SpMM and epilogue callables are injectable so that the CPU tests drive the same schedule over
 gloo with an oracle SpMM.
@@ -395,10 +397,15 @@ class ShardedPropagation:
             # push: item partial sums from this rank's users at layer k-1, chunk by chunk, each
             # chunk's exchange issued as soon as its launch is queued
             ex = []
+            blocking = rec is not None and self._collective and not self._a2a_native
             for Ac, c0, m in self.push_chunks:
                 self.layer_fn(Ac, self.Xu[k - 1], _lib.LGX_LAYER_PARTIAL,
                               out=self._chunk_views(c0, m)[0].view(s.world * m, self.d))
+                if blocking:
+                    rec.mark("push")
                 ex.append(self._exchange(c0, m))
+                if blocking:  # gloo: the exchange returned on the host only once done
+                    rec.mark("exchange_sync")
             if rec:
                 rec.mark("push")
             # pull: this rank's user rows from the full item table of layer k-1
@@ -437,12 +444,14 @@ class ShardedPropagation:
 
     def phase_summary(self) -> Dict[str, float]:
         """Mean ms per recorded step by phase, plus comm_exposed_ms = allgather_wait +
-        exchange_wait (the stream's time behind collectives).  Synchronises the device."""
+        exchange_wait + exchange_sync (the stream's time behind collectives).  Synchronises the
+        device."""
         if self.phases.cuda:
             torch.cuda.synchronize()
         ph = self.phases.summary()
         ph.pop("begin", None)
-        ph["comm_exposed_ms"] = ph.get("allgather_wait", 0.0) + ph.get("exchange_wait", 0.0)
+        ph["comm_exposed_ms"] = ph.get("allgather_wait", 0.0) + ph.get("exchange_wait", 0.0) + \
+            ph.get("exchange_sync", 0.0)
         return ph
 
     def gather_outputs(self) -> Tuple[torch.Tensor, torch.Tensor]:

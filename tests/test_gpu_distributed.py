@@ -57,6 +57,8 @@ def _worker(rank, world, port, K, dtype_name, q, backend="gloo"):
             prop.step()
             ph = prop.phase_summary()
             assert ph["push"] > 0 and ph["pull"] > 0 and ph["comm_exposed_ms"] >= 0, ph
+            if not prop._a2a_native and prop._collective:  # gloo: host-synchronous exchanges, stamped apart
+                assert ph["exchange_sync"] >= 0 and ph["comm_exposed_ms"] >= ph["exchange_sync"], ph
             ou, oi = prop.gather_outputs()
             outs.append((ou.clone(), oi.clone()))
         torch.cuda.synchronize()
