@@ -56,9 +56,13 @@ def test_one_batch(rating_k: np.ndarray, ground_true: Sequence[Sequence[int]], t
     """Procedure.test_one_batch (Procedure.py:60-72) with RecallPrecision_ATk / NDCGatK_r
     (code/utils.py:218-262), vectorised over users: the same float64 arrays as the reference's
     per-user loops, reduced in the same order, so the sums are identical."""
-    r = _label(ground_true, rating_k)
-    pre, rec, ndcg = [], [], []
     recall_n = np.fromiter(map(len, ground_true), dtype=np.int64, count=len(ground_true))
+    return _metrics(_label(ground_true, rating_k), recall_n, topks)
+
+
+def _metrics(r: np.ndarray, recall_n: np.ndarray, topks: Sequence[int]) -> Dict:
+    """RecallPrecision_ATk / NDCGatK_r sums over a batch from its hit matrix r (float64 0/1)."""
+    pre, rec, ndcg = [], [], []
     for k in topks:
         right = r[:, :k].sum(1)
         rec.append(np.sum(right / recall_n))
@@ -73,26 +77,62 @@ def test_one_batch(rating_k: np.ndarray, ground_true: Sequence[Sequence[int]], t
     return {"recall": np.array(rec), "precision": np.array(pre), "ndcg": np.array(ndcg)}
 
 
+class _TestLists:
+    """The static lists of one evaluation set on the device: the test users (row ids), their train
+    positives (the mask CSR) and their test items as sorted (row * M + item) keys.  Procedure.Test
+    runs every few epochs over the same testDict / allPos; building these from Python lists was most
+    of its time (profiles/r04_rows.json, a7 phases), so they are kept for as long as the same
+    testDict object is passed (the reference never mutates it after loading, dataloader.py:282-293)."""
+
+    _cache: Dict[tuple, "_TestLists"] = {}
+
+    def __init__(self, dataset, testDict, n_items: int, dev):
+        self.testDict = testDict  # held: its id cannot be reused while cached
+        self.users = list(testDict.keys())
+        n = len(self.users)
+        self.rows = torch.as_tensor(self.users, dtype=torch.int64, device=dev)
+        self.mask = ops.lists_to_device_csr(dataset.getUserPosItems(self.users), dev, sort=True)
+        truths = [testDict[u] for u in self.users]
+        self.recall_n = np.fromiter(map(len, truths), dtype=np.int64, count=n)
+        flat = np.fromiter(itertools.chain.from_iterable(truths), dtype=np.int64, count=int(self.recall_n.sum()))
+        self.M = int(max(n_items, int(flat.max()) + 1 if flat.size else 0, 1))
+        keys = np.repeat(np.arange(n, dtype=np.int64), self.recall_n) * self.M + flat
+        self.keys = torch.unique(torch.from_numpy(keys).to(dev))  # sorted
+
+    @classmethod
+    def get(cls, dataset, n_items: int, dev) -> "_TestLists":
+        td = dataset.testDict
+        key = (id(dataset), id(td), len(td), n_items, str(dev))
+        hit = cls._cache.get(key)
+        if hit is None or hit.testDict is not td:
+            cls._cache.clear()
+            hit = cls._cache[key] = cls(dataset, td, n_items, dev)
+        return hit
+
+    def hits(self, idx: torch.Tensor) -> np.ndarray:
+        """utils.getLabel on the device: r[i, j] = 1.0 if idx[i, j] is a test item of user i."""
+        if self.keys.numel() == 0:
+            return np.zeros(tuple(idx.shape), dtype=float)
+        q = torch.arange(idx.shape[0], device=idx.device, dtype=torch.int64)[:, None] * self.M + idx.long()
+        pos = torch.searchsorted(self.keys, q.reshape(-1)).clamp_(max=self.keys.numel() - 1).view_as(q)
+        return ((self.keys[pos] == q) & (idx >= 0)).to(torch.uint8).cpu().numpy().astype(float)
+
+
 def Test(dataset, Recmodel, epoch=0, w=None, multicore=0, topks: Sequence[int] = (20,)) -> Dict:
     """Procedure.Test on the fused engine: one propagation, one fused score+mask+top-k launch for
-    all test users (sigmoid scores, positives set to -(1<<10) as Procedure.py:134)."""
-    testDict: Dict[int, List[int]] = dataset.testDict
+    all test users (sigmoid scores, positives set to -(1<<10) as Procedure.py:134), the hit matrix
+    on the device, the metric sums on the host in the reference's float64 order."""
     Recmodel = Recmodel.eval()
     max_K = max(topks)
     results = {"precision": np.zeros(len(topks)), "recall": np.zeros(len(topks)), "ndcg": np.zeros(len(topks))}
     with torch.no_grad():
-        users = list(testDict.keys())
         all_users, all_items = Recmodel.computer()
-        dev = all_users.device
-        allPos = dataset.getUserPosItems(users)
-        mask = ops.lists_to_device_csr(allPos, dev, sort=True)
-        rows = torch.as_tensor(users, dtype=torch.int64, device=dev)
-        idx, _ = ops.score_topk(all_users, all_items, max_K, user_rows=rows, mask=mask,
+        tl = _TestLists.get(dataset, all_items.shape[0], all_users.device)
+        idx, _ = ops.score_topk(all_users, all_items, max_K, user_rows=tl.rows, mask=tl.mask,
                                 mask_value=-float(1 << 10), apply_sigmoid=True)
-        rating_k = idx.cpu().numpy()
-        res = test_one_batch(rating_k, [testDict[u] for u in users], topks)
+        res = _metrics(tl.hits(idx), tl.recall_n, topks)
         for key in results:
-            results[key] = res[key] / float(len(users))
+            results[key] = res[key] / float(len(tl.users))
     return results
 
 
