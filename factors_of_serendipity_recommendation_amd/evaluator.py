@@ -137,6 +137,38 @@ def Test(dataset, Recmodel, epoch=0, w=None, multicore=0, topks: Sequence[int] =
 
 
 # --------------------------------------------------------------------------- TF batch_test
+class _BatchLists:
+    """batch_test's per-user lists on the device: row ids, the train-item mask (flag 0) and the
+    truth lists, built once for a given (users, train_items, test_set, flag) and reused while the
+    same dict objects and the same users come back (the reference's data_generator holds them for
+    the whole run, batch_test.py:12-23)."""
+
+    _cache: Dict[tuple, "_BatchLists"] = {}
+
+    def __init__(self, users: np.ndarray, train_items, test_set, flag: int, dev):
+        self.train_items, self.test_set, self.users = train_items, test_set, users  # held (ids stay valid)
+        ul = users.tolist()
+        self.rows = torch.as_tensor(users, dtype=torch.int64, device=dev)
+        if flag == 0:
+            truths = [test_set[u] for u in ul]
+            self.mask = ops.lists_to_device_csr([train_items[u] for u in ul], dev, sort=True)  # KeyError as :64
+        else:
+            truths = [train_items[u] for u in ul]
+            self.mask = None
+        self.truth = ops.lists_to_device_csr(truths, dev, sort=False)
+
+    @classmethod
+    def get(cls, users_to_test, train_items, test_set, flag: int, dev) -> "_BatchLists":
+        users = np.fromiter((int(u) for u in users_to_test), dtype=np.int64)
+        key = (id(train_items), id(test_set), len(users), flag, str(dev))
+        hit = cls._cache.get(key)
+        if (hit is None or hit.train_items is not train_items or hit.test_set is not test_set
+                or not np.array_equal(hit.users, users)):
+            cls._cache.clear()
+            hit = cls._cache[key] = cls(users, train_items, test_set, flag, dev)
+        return hit
+
+
 def batch_test(user_emb: torch.Tensor, item_emb: torch.Tensor, users_to_test: Sequence[int],
                train_items: Dict[int, Sequence[int]], test_set: Dict[int, Sequence[int]],
                Ks: Sequence[int] = (20,), train_set_flag: int = 0) -> Dict:
@@ -145,17 +177,9 @@ def batch_test(user_emb: torch.Tensor, item_emb: torch.Tensor, users_to_test: Se
     (train_set_flag=1, :66-68); top-max(Ks), fold-out curves, float32 mean over users."""
     top_show = np.sort(np.asarray(Ks))
     max_top = int(max(top_show))
-    dev = user_emb.device
-    users = [int(u) for u in users_to_test]
-    rows = torch.as_tensor(users, dtype=torch.int64, device=dev)
-    if train_set_flag == 0:
-        truths = [test_set[u] for u in users]
-        mask = ops.lists_to_device_csr([train_items[u] for u in users], dev, sort=True)  # KeyError as :64
-    else:
-        truths = [train_items[u] for u in users]
-        mask = None
-    idx, _ = ops.score_topk(user_emb, item_emb, max_top, user_rows=rows, mask=mask, mask_value=float("-inf"))
-    curves = ops.foldout_metrics(idx, ops.lists_to_device_csr(truths, dev, sort=False)).cpu().numpy()
+    bl = _BatchLists.get(users_to_test, train_items, test_set, train_set_flag, user_emb.device)
+    idx, _ = ops.score_topk(user_emb, item_emb, max_top, user_rows=bl.rows, mask=bl.mask, mask_value=float("-inf"))
+    curves = ops.foldout_metrics(idx, bl.truth).cpu().numpy()
     final = np.mean(curves, axis=0).reshape(5, max_top)[:, top_show - 1].reshape(5, len(top_show))
     return {"precision": final[0].astype(np.float64), "recall": final[1].astype(np.float64),
             "ndcg": final[3].astype(np.float64)}
