@@ -2,7 +2,7 @@
 items per user) timed with HIP events; run under rocprofv3 --kernel-trace --stats for the per-kernel
 split (floor pass, the seeded stages, the split tail, the finalize).
 
-  python tools/score_probe.py [B] [dtype]
+  python tools/score_probe.py [B] [dtype] [--lib other/liblgx.so]   (--lib: time another build)
 """
 import os
 import sys
@@ -12,7 +12,13 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import factors_of_serendipity_recommendation_amd as lgx  # noqa: E402
-from factors_of_serendipity_recommendation_amd import ops  # noqa: E402
+from factors_of_serendipity_recommendation_amd import _lib, ops  # noqa: E402
+
+if "--lib" in sys.argv:
+    j = sys.argv.index("--lib")
+    _lib.LIB_PATH = os.path.abspath(sys.argv[j + 1])
+    _lib._lib = None
+    del sys.argv[j:j + 2]
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 262144
 dt = torch.float32 if len(sys.argv) > 2 and sys.argv[2] == "f32" else torch.bfloat16
