@@ -92,11 +92,6 @@ class _TestLists:
         n = len(self.users)
         self.rows = torch.as_tensor(self.users, dtype=torch.int64, device=dev)
         self.mask = ops.lists_to_device_csr(dataset.getUserPosItems(self.users), dev, sort=True)
-        ip, ix = self.mask
-        # the same entries as (user position, item) pairs, for the dense route's -inf scatter
-        self.mask_flat = (torch.repeat_interleave(torch.arange(n, device=dev), ip[1:] - ip[:-1]) * int(n_items)
-                          + ix.to(torch.int64)) if ix.numel() else None
-        self.mask_ip_host = ip.cpu().numpy()
         truths = [testDict[u] for u in self.users]
         self.recall_n = np.fromiter(map(len, truths), dtype=np.int64, count=n)
         flat = np.fromiter(itertools.chain.from_iterable(truths), dtype=np.int64, count=int(self.recall_n.sum()))
@@ -123,45 +118,6 @@ class _TestLists:
         return ((self.keys[pos] == q) & (idx >= 0)).to(torch.uint8).cpu().numpy().astype(float)
 
 
-# Procedure.Test's ranking route.  Up to _DENSE_MAX_ITEMS items the users' raw scores are written in
-# slabs of at most _DENSE_SLAB_BYTES (lgx_score_dense), the train positives set to -inf and each row's
-# top-k taken by lgx_topk_rows: at these catalog sizes a streaming top-k meets an insertion in
-# almost every 64-item tile of every wave (k ln(n / k) per user), so the fused launch runs its
-# exact event path throughout, while the two passes are bounded by the MFMAs and one write + one read
-# of the slab (Gowalla shape: profiles/r04_rows.json).  Both routes rank by the raw score with ties
-# to the lower item and put masked items last in ascending order, so they return the same lists up
-# to the rounding of the two walks' fp32 sums.  Larger catalogs take the fused launch.
-_DENSE_MAX_ITEMS = 1 << 18
-_DENSE_MIN_USERS = 1024
-_DENSE_SLAB_BYTES = 4 << 30
-
-
-def _rank_dense(all_users: torch.Tensor, all_items: torch.Tensor, tl: "_TestLists", k: int) -> torch.Tensor:
-    B, I = tl.rows.numel(), all_items.shape[0]
-    chunk = max(1, min(B, _DENSE_SLAB_BYTES // (4 * I)))
-    out = torch.empty((B, k), dtype=torch.int32, device=all_users.device)
-    ip = tl.mask_ip_host
-    for c0 in range(0, B, chunk):
-        c1 = min(B, c0 + chunk)
-        S = ops.score_dense(all_users, all_items, user_rows=tl.rows[c0:c1])
-        if tl.mask_flat is not None:
-            e0, e1 = int(ip[c0]), int(ip[c1])  # this chunk's mask entries are contiguous
-            if e1 > e0:
-                S.view(-1).index_fill_(0, tl.mask_flat[e0:e1] - c0 * I, float("-inf"))
-        out[c0:c1] = ops.topk_rows(S, k)[0]
-        del S
-    return out
-
-
-def _rank(all_users: torch.Tensor, all_items: torch.Tensor, tl: "_TestLists", k: int) -> torch.Tensor:
-    """The test users' top-k item ids with their train positives excluded (Procedure.py:127-135)."""
-    I = all_items.shape[0]
-    if k <= I <= _DENSE_MAX_ITEMS and tl.rows.numel() >= _DENSE_MIN_USERS:
-        return _rank_dense(all_users, all_items, tl, k)
-    return ops.score_topk(all_users, all_items, k, user_rows=tl.rows, mask=tl.mask,
-                          mask_value=-float(1 << 10), apply_sigmoid=True)[0]
-
-
 def Test(dataset, Recmodel, epoch=0, w=None, multicore=0, topks: Sequence[int] = (20,)) -> Dict:
     """Procedure.Test on the fused engine: one propagation, one fused score+mask+top-k launch for
     all test users (sigmoid scores, positives set to -(1<<10) as Procedure.py:134), the hit matrix
@@ -172,7 +128,8 @@ def Test(dataset, Recmodel, epoch=0, w=None, multicore=0, topks: Sequence[int] =
     with torch.no_grad():
         all_users, all_items = Recmodel.computer()
         tl = _TestLists.get(dataset, all_items.shape[0], all_users.device)
-        idx = _rank(all_users, all_items, tl, max_K)
+        idx, _ = ops.score_topk(all_users, all_items, max_K, user_rows=tl.rows, mask=tl.mask,
+                                mask_value=-float(1 << 10), apply_sigmoid=True)
         res = _metrics(tl.hits(idx), tl.recall_n, topks)
         for key in results:
             results[key] = res[key] / float(len(tl.users))

@@ -481,7 +481,7 @@ def row_eval(rows, reps, tmpdir, cfg_name):
     # time and its phase split come from the same runs
     # (the first call above built the test lists -- row ids, mask CSR, test-item keys -- once; a later
     # Procedure.Test call over the same testDict reuses them, as these do)
-    ph = {"propagation": [], "lists": [], "rank": [], "hits_metrics": []}
+    ph = {"propagation": [], "lists": [], "score_topk": [], "hits_metrics": []}
     walls = []
     for _ in range(reps):
         model._eval_cache = None
@@ -491,25 +491,17 @@ def row_eval(rows, reps, tmpdir, cfg_name):
         t1 = sync_t()
         tl = evaluator._TestLists.get(ds, all_items.shape[0], all_users.device)
         t2 = sync_t()
-        idx = evaluator._rank(all_users, all_items, tl, 20)
+        idx, _ = ops.score_topk(all_users, all_items, 20, user_rows=tl.rows, mask=tl.mask,
+                                mask_value=-float(1 << 10), apply_sigmoid=True)
         t3 = sync_t()
         evaluator._metrics(tl.hits(idx), tl.recall_n, [20])
         t4 = sync_t()
-        for k_, a_, b_ in (("propagation", t0, t1), ("lists", t1, t2), ("rank", t2, t3),
+        for k_, a_, b_ in (("propagation", t0, t1), ("lists", t1, t2), ("score_topk", t2, t3),
                            ("hits_metrics", t3, t4)):
             ph[k_].append((b_ - a_) * 1e3)
         walls.append(t4 - t0)
     ph = {k_: float(np.median(v)) for k_, v in ph.items()}
     ms = float(np.median(walls)) * 1e3
-    route = "dense slabs + row top-k" if (20 <= all_items.shape[0] <= evaluator._DENSE_MAX_ITEMS
-                                          and tl.rows.numel() >= evaluator._DENSE_MIN_USERS) else "fused launch"
-    tf = []
-    for _ in range(reps):
-        t0 = sync_t()
-        ops.score_topk(all_users, all_items, 20, user_rows=tl.rows, mask=tl.mask, mask_value=-float(1 << 10),
-                       apply_sigmoid=True)
-        tf.append(sync_t() - t0)
-    fused_ms = float(np.median(tf)) * 1e3
     # CPU: Procedure.Test's per-batch body on the host (computer() + getUsersRating + mask + topk +
     # test_one_batch), 3 batches of 100 users, extrapolated to ceil(n_test / 100) batches
     A = model._csr
@@ -536,7 +528,6 @@ def row_eval(rows, reps, tmpdir, cfg_name):
          f"{cfg.n_users} x {cfg.n_items}, {A.nnz} nnz, K={cfg.K}, d={cfg.d} fp32, {n_test} test users; phases (ms): "
          + ", ".join(f"{k_} {v:.2f}" for k_, v in ph.items())
          + f"; host share (lists + hits / metric sums) {(ph['lists'] + ph['hits_metrics']) / sum(ph.values()):.2f}; "
-           f"rank route: {route} (the fused launch alone: {fused_ms:.2f} ms); "
            f"recall@20 {float(res['recall'][0]):.5f} (synthetic graph)")
     rows[-1]["roofline"] = {"bound": "latency", "note": "end-to-end loop: phases above; kernels have their own rows"}
     rows[-1]["phases_ms"] = ph
