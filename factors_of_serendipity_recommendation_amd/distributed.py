@@ -378,7 +378,8 @@ class ShardedPropagation:
         return dist.all_gather_into_tensor(table, self.send_i, group=self.group, async_op=True)
 
     def schedule(self) -> List[Tuple[str, int]]:
-        """Per layer: push (items) + reduce-scatter, pull (users), item epilogue + all-gather."""
+        """Per layer: push (items, chunked, each chunk exchanged), pull (users), item sums + epilogue +
+        all-gather."""
         order = []
         for k in range(1, self.K + 1):
             order.extend([("push", k), ("pull", k), ("items", k)])
