@@ -295,3 +295,32 @@ def test_column_blocks_cover_item_rows_once(nb):
     assert A.col_block_count(4, 4) == nb
     cs = A.c_struct(4, 4)
     assert cs.cb_n == nb and cs.cb_row0 == U and cs.n_segs == blk["n_user_segs"]
+
+
+def test_test_lists_cache_and_hits_match_get_label():
+    """evaluator._TestLists (host-side logic, CPU tensors): reused while the same testDict object
+    comes back, rebuilt for a new one; its hit matrix equals utils.getLabel's restatement (_label),
+    padding ids (-1) never hit."""
+    from factors_of_serendipity_recommendation_amd import evaluator
+    rng = np.random.default_rng(4)
+    n_items = 300
+
+    class DS:
+        def __init__(self):
+            self.testDict = {u: sorted(rng.choice(n_items, rng.integers(1, 9), replace=False).tolist())
+                             for u in rng.choice(1000, 64, replace=False).tolist()}
+            self._pos = {u: sorted(rng.choice(n_items, 5, replace=False).tolist()) for u in self.testDict}
+
+        def getUserPosItems(self, users):
+            return [self._pos[u] for u in users]
+
+    ds = DS()
+    a = evaluator._TestLists.get(ds, n_items, torch.device("cpu"))
+    assert evaluator._TestLists.get(ds, n_items, torch.device("cpu")) is a
+    pred = rng.integers(-1, n_items, (len(a.users), 20))
+    pred[:, 0] = [ds.testDict[u][0] for u in a.users]  # at least one hit per user
+    got = a.hits(torch.from_numpy(pred))
+    ref = evaluator._label([ds.testDict[u] for u in a.users], np.maximum(pred, 0)) * (pred >= 0)
+    assert np.array_equal(got, ref) and got[:, 0].all()
+    ds.testDict = dict(ds.testDict)  # a new object: rebuilt
+    assert evaluator._TestLists.get(ds, n_items, torch.device("cpu")) is not a
