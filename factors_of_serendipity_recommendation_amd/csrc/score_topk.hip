@@ -144,6 +144,11 @@ constexpr int kListSpare = 8;  // the 8-key rescan of user 31 may read past its 
 // ring's depth measured neutral) and fit d = 256 up to k = 20.
 constexpr int kPendSlots = 4;
 constexpr int kPendBf16Lds = 12;
+// deferred slots of the LDS walk: 12 for bf16, and for fp32 up to d = 128, whose tiles leave the LDS
+// for them; fp32 at d = 256 keeps 4 (two 64 KB tiles and four waves' lists fill the 160 KB).  fp32
+// with 12 (profiles/r04_eval_probe_ab.txt, masked top-20): Gowalla shape 3.67 -> 3.30 ms, Amazon-book
+// shape 17.6 -> 16.6 ms
+__host__ __device__ constexpr int lds_pend(bool f32, int ksteps) { return f32 && ksteps > 8 ? kPendSlots : kPendBf16Lds; }
 __host__ __device__ constexpr size_t list_keys_per_wave(int k) { return (size_t)kUsersPerWave * kstride(k) + kListSpare; }
 // ... then one int per lane: the count of its parked keys (kSuspSlots)
 __host__ __device__ constexpr size_t list_bytes_per_wave(int k, int pend = kPendSlots) {
@@ -792,7 +797,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5, col = lane & 31;
-    typedef WaveTopKT<F32 ? kPendSlots : kPendBf16Lds> TopK;
+    typedef WaveTopKT<lds_pend(F32, KSTEPS)> TopK;
     uint64_t* lk = reinterpret_cast<uint64_t*>(smem + (size_t)nbuf * G::TILE + (size_t)wave * list_bytes_per_wave(k, TopK::kPend));
 
     // workgroup -> (catalog split, user tile)
@@ -1660,7 +1665,8 @@ bool lds_eligible(int dtype, int64_t d, int k) {
         return d % 32 == 0 && d >= 32 && d <= 256 && k <= 32 &&
                2 * (size_t)kTileItems * d * 2 + 8 * list_bytes_per_wave(k, kPendBf16Lds) <= kLdsBytes;
     if (dtype != LGX_DTYPE_F32 || d % 64 != 0 || d < 64 || d > 256 || k > 32) return false;
-    return 2 * (size_t)kTileItems * d * 4 + (size_t)kF32LdsWaves * list_bytes_per_wave(k) <= kLdsBytes;
+    return 2 * (size_t)kTileItems * d * 4 + (size_t)kF32LdsWaves * list_bytes_per_wave(k, lds_pend(true, (int)(d / 16))) <=
+           kLdsBytes;
 }
 
 SplitPlan plan_splits(int64_t B, int64_t n_items, int dtype, int64_t d, int k) {
@@ -1761,7 +1767,7 @@ int launch_bf16_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t s
 template <int KS, bool MM, int MODE>
 int launch_f32_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     typedef LdsGeom<KS, kF32LdsWaves, 2, 4> G;
-    const size_t lists = (size_t)kF32LdsWaves * list_bytes_per_wave(a.k);
+    const size_t lists = (size_t)kF32LdsWaves * list_bytes_per_wave(a.k, lds_pend(true, KS));
     const int nbuf = lds_ring_buffers(G::TILE, lists, 1);
     const size_t shmem = (size_t)nbuf * G::TILE + lists;
     if (shmem > kLdsBytes) {
@@ -1843,8 +1849,11 @@ int plan_ranges(int64_t B, int64_t n_items, int dtype, int64_t d, int k, UserRan
     const int64_t resident = lds_resident();
     if (p.lds && p.n_splits == 1 && p.n_utiles >= resident) {  // full-sweep mode
         const int64_t rem_tiles = p.n_utiles % resident;
-        // measured: a 67-tile tail (of 256) runs faster as a split launch, a 135-tile one slower
-        if (rem_tiles != 0 && rem_tiles * 100 < resident * 35) full = (p.n_utiles - rem_tiles) * p.waves * kUsersPerWave;
+        // measured: a 67-tile tail (of 256) runs faster as a split launch, a 135-tile one slower (bf16,
+        // C5); fp32 tiles are 16x longer per event, and a 156-tile tail of the Amazon-book shape runs
+        // 9 % faster split (profiles/r04_eval_probe_ab.txt)
+        const int64_t cut = dtype == LGX_DTYPE_F32 ? 75 : 35;
+        if (rem_tiles != 0 && rem_tiles * 100 < resident * cut) full = (p.n_utiles - rem_tiles) * p.waves * kUsersPerWave;
     }
     size_t off = 0;
     r[n++] = {0, full, plan_splits(full, n_items, dtype, d, k), 0};
