@@ -60,6 +60,28 @@ def test_one_batch(rating_k: np.ndarray, ground_true: Sequence[Sequence[int]], t
     return _metrics(_label(ground_true, rating_k), recall_n, topks)
 
 
+def _metrics_dev(hit: torch.Tensor, recall_n: torch.Tensor, topks: Sequence[int]) -> Dict:
+    """_metrics on the device in float64: the same per-user terms (getLabel's 0 / 1, right / len,
+    dcg / idcg with 1 / log2(j + 2)), summed over users by torch instead of numpy -- the sums agree to
+    float64 rounding (the reference itself adds them batch by batch, Procedure.py:159-163)."""
+    r = hit.to(torch.float64)
+    n = recall_n.to(torch.float64)
+    out = {"recall": [], "precision": [], "ndcg": []}
+    for k in topks:
+        right = r[:, :k].sum(1)
+        out["recall"].append(torch.sum(right / n))
+        out["precision"].append(torch.sum(right) / k)
+        w = 1.0 / torch.log2(torch.arange(2, k + 2, device=r.device, dtype=torch.float64))
+        tm = (torch.arange(k, device=r.device)[None, :] < torch.clamp(recall_n, max=k)[:, None]).to(torch.float64)
+        idcg = torch.sum(tm * w, dim=1)
+        dcg = torch.sum(r[:, :k] * w, dim=1)
+        idcg[idcg == 0.] = 1.
+        nd = dcg / idcg
+        nd[torch.isnan(nd)] = 0.
+        out["ndcg"].append(torch.sum(nd))
+    return {key: torch.stack(v).cpu().numpy() for key, v in out.items()}
+
+
 def _metrics(r: np.ndarray, recall_n: np.ndarray, topks: Sequence[int]) -> Dict:
     """RecallPrecision_ATk / NDCGatK_r sums over a batch from its hit matrix r (float64 0/1)."""
     pre, rec, ndcg = [], [], []
@@ -94,6 +116,7 @@ class _TestLists:
         self.mask = ops.lists_to_device_csr(dataset.getUserPosItems(self.users), dev, sort=True)
         truths = [testDict[u] for u in self.users]
         self.recall_n = np.fromiter(map(len, truths), dtype=np.int64, count=n)
+        self.recall_n_dev = torch.from_numpy(self.recall_n).to(dev)
         flat = np.fromiter(itertools.chain.from_iterable(truths), dtype=np.int64, count=int(self.recall_n.sum()))
         self.M = int(max(n_items, int(flat.max()) + 1 if flat.size else 0, 1))
         keys = np.repeat(np.arange(n, dtype=np.int64), self.recall_n) * self.M + flat
@@ -109,13 +132,17 @@ class _TestLists:
             hit = cls._cache[key] = cls(dataset, td, n_items, dev)
         return hit
 
-    def hits(self, idx: torch.Tensor) -> np.ndarray:
-        """utils.getLabel on the device: r[i, j] = 1.0 if idx[i, j] is a test item of user i."""
+    def hit_mask(self, idx: torch.Tensor) -> torch.Tensor:
+        """utils.getLabel on the device: bool [n, k], True where idx[i, j] is a test item of user i."""
         if self.keys.numel() == 0:
-            return np.zeros(tuple(idx.shape), dtype=float)
+            return torch.zeros(tuple(idx.shape), dtype=torch.bool, device=idx.device)
         q = torch.arange(idx.shape[0], device=idx.device, dtype=torch.int64)[:, None] * self.M + idx.long()
         pos = torch.searchsorted(self.keys, q.reshape(-1)).clamp_(max=self.keys.numel() - 1).view_as(q)
-        return ((self.keys[pos] == q) & (idx >= 0)).to(torch.uint8).cpu().numpy().astype(float)
+        return (self.keys[pos] == q) & (idx >= 0)
+
+    def hits(self, idx: torch.Tensor) -> np.ndarray:
+        """The hit matrix as getLabel returns it (float64 0 / 1, on the host)."""
+        return self.hit_mask(idx).to(torch.uint8).cpu().numpy().astype(float)
 
 
 def Test(dataset, Recmodel, epoch=0, w=None, multicore=0, topks: Sequence[int] = (20,)) -> Dict:
@@ -130,7 +157,7 @@ def Test(dataset, Recmodel, epoch=0, w=None, multicore=0, topks: Sequence[int] =
         tl = _TestLists.get(dataset, all_items.shape[0], all_users.device)
         idx, _ = ops.score_topk(all_users, all_items, max_K, user_rows=tl.rows, mask=tl.mask,
                                 mask_value=-float(1 << 10), apply_sigmoid=True)
-        res = _metrics(tl.hits(idx), tl.recall_n, topks)
+        res = _metrics_dev(tl.hit_mask(idx), tl.recall_n_dev, topks)
         for key in results:
             results[key] = res[key] / float(len(tl.users))
     return results

@@ -324,3 +324,17 @@ def test_test_lists_cache_and_hits_match_get_label():
     assert np.array_equal(got, ref) and got[:, 0].all()
     ds.testDict = dict(ds.testDict)  # a new object: rebuilt
     assert evaluator._TestLists.get(ds, n_items, torch.device("cpu")) is not a
+
+
+def test_device_metric_sums_match_host_sums():
+    """evaluator._metrics_dev (torch float64, CPU tensors here) equals the host restatement
+    _metrics to float64 rounding, users with fewer test items than k included."""
+    from factors_of_serendipity_recommendation_amd import evaluator
+    rng = np.random.default_rng(9)
+    n, K = 3000, 100
+    hit = rng.random((n, K)) < 0.05
+    recall_n = rng.integers(1, 40, n)
+    host = evaluator._metrics(hit.astype(float), recall_n, [1, 5, 20, 100])
+    dev = evaluator._metrics_dev(torch.from_numpy(hit), torch.from_numpy(recall_n), [1, 5, 20, 100])
+    for key in ("recall", "precision", "ndcg"):
+        assert np.allclose(dev[key], host[key], rtol=1e-13, atol=0), key

@@ -494,7 +494,7 @@ def row_eval(rows, reps, tmpdir, cfg_name):
         idx, _ = ops.score_topk(all_users, all_items, 20, user_rows=tl.rows, mask=tl.mask,
                                 mask_value=-float(1 << 10), apply_sigmoid=True)
         t3 = sync_t()
-        evaluator._metrics(tl.hits(idx), tl.recall_n, [20])
+        evaluator._metrics_dev(tl.hit_mask(idx), tl.recall_n_dev, [20])
         t4 = sync_t()
         for k_, a_, b_ in (("propagation", t0, t1), ("lists", t1, t2), ("score_topk", t2, t3),
                            ("hits_metrics", t3, t4)):
