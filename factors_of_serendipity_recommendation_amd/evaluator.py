@@ -206,7 +206,10 @@ def batch_test(user_emb: torch.Tensor, item_emb: torch.Tensor, users_to_test: Se
     max_top = int(max(top_show))
     bl = _BatchLists.get(users_to_test, train_items, test_set, train_set_flag, user_emb.device)
     idx, _ = ops.score_topk(user_emb, item_emb, max_top, user_rows=bl.rows, mask=bl.mask, mask_value=float("-inf"))
-    curves = ops.foldout_metrics(idx, bl.truth).cpu().numpy()
-    final = np.mean(curves, axis=0).reshape(5, max_top)[:, top_show - 1].reshape(5, len(top_show))
+    curves = ops.foldout_metrics(idx, bl.truth)
+    # the users' mean on the device (summed in float64, rounded to float32 once): only 5 x max_top
+    # values cross to the host
+    mean = (curves.double().sum(0) / max(1, curves.shape[0])).float().cpu().numpy()
+    final = mean.reshape(5, max_top)[:, top_show - 1].reshape(5, len(top_show))
     return {"precision": final[0].astype(np.float64), "recall": final[1].astype(np.float64),
             "ndcg": final[3].astype(np.float64)}
