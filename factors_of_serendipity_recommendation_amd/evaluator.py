@@ -148,7 +148,7 @@ class _TestLists:
 def Test(dataset, Recmodel, epoch=0, w=None, multicore=0, topks: Sequence[int] = (20,)) -> Dict:
     """Procedure.Test on the fused engine: one propagation, one fused score+mask+top-k launch for
     all test users (sigmoid scores, positives set to -(1<<10) as Procedure.py:134), the hit matrix
-    on the device, the metric sums on the host in the reference's float64 order."""
+    and the float64 metric sums on the device."""
     Recmodel = Recmodel.eval()
     max_K = max(topks)
     results = {"precision": np.zeros(len(topks)), "recall": np.zeros(len(topks)), "ndcg": np.zeros(len(topks))}
