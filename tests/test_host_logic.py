@@ -338,3 +338,25 @@ def test_device_metric_sums_match_host_sums():
     dev = evaluator._metrics_dev(torch.from_numpy(hit), torch.from_numpy(recall_n), [1, 5, 20, 100])
     for key in ("recall", "precision", "ndcg"):
         assert np.allclose(dev[key], host[key], rtol=1e-13, atol=0), key
+
+
+def test_batch_lists_cache_reuse_and_invalidation():
+    """evaluator._BatchLists (CPU tensors): reused for the same dicts and users, rebuilt when the
+    users, a dict object or the flag change; flag 1 has no mask and takes the train items as truth."""
+    from factors_of_serendipity_recommendation_amd import evaluator
+    rng = np.random.default_rng(2)
+    train = {u: sorted(rng.choice(500, 6, replace=False).tolist()) for u in range(40)}
+    test = {u: sorted(rng.choice(500, 3, replace=False).tolist()) for u in range(40)}
+    dev = torch.device("cpu")
+    users = list(range(0, 40, 2))
+    a = evaluator._BatchLists.get(users, train, test, 0, dev)
+    assert evaluator._BatchLists.get(list(users), train, test, 0, dev) is a
+    ip, ix = a.mask
+    assert ix[ip[1]:ip[2]].tolist() == train[users[1]]
+    b = evaluator._BatchLists.get(users[::-1], train, test, 0, dev)
+    assert b is not a and b.rows.tolist() == users[::-1]
+    c = evaluator._BatchLists.get(users[::-1], dict(train), test, 0, dev)
+    assert c is not b
+    f1 = evaluator._BatchLists.get(users, train, test, 1, dev)
+    tp, tx = f1.truth
+    assert f1.mask is None and tx[tp[0]:tp[1]].tolist() == train[users[0]]
