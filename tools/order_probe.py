@@ -4,7 +4,7 @@ propagates them with the LightGCN module, and times lgx_score_topk (masked top-2
 on the item table as is and with its rows permuted by descending norm (timing only: the permuted
 call's ids are in the permuted space).  HIP events, median of 5.
 
-  python tools/order_probe.py
+  python tools/order_probe.py [--lib other/liblgx.so]
 """
 import os
 import sys
@@ -15,7 +15,11 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
 import bench_rows as br  # noqa: E402
-from factors_of_serendipity_recommendation_amd import evaluator, ops  # noqa: E402
+from factors_of_serendipity_recommendation_amd import _lib, evaluator, ops  # noqa: E402
+
+if "--lib" in sys.argv:
+    _lib.LIB_PATH = os.path.abspath(sys.argv[sys.argv.index("--lib") + 1])
+    _lib._lib = None
 from factors_of_serendipity_recommendation_amd.model import LightGCN  # noqa: E402
 
 
