@@ -2,6 +2,9 @@
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config synth10m] [--score-users 1000000]
   N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+       or just `python bench.py --gpus N`: without WORLD_SIZE in the environment it starts the N
+       ranks itself (torch.distributed.run as a child process) and forwards rank 0's line; a
+       WORLD_SIZE that differs from --gpus is an error (exit 2), never a silent one-rank run.
 
 Workload (BASELINE.json): the propagation metric is quoted at 1/2/4/8 GPUs on configs[3]
 ("Synthetic 10M users x 1M items, 500M edges, K=3, d=128, row-sharded with RCCL all-gather"),
@@ -11,8 +14,8 @@ total graph is fixed as N grows (strong scaling).  One step = one full K-layer p
 reference's precision (model.py:163-176); the same line carries the bf16-storage / fp32-accumulate
 run ("fp32 parity; bf16 perf") under "bf16".  The scoring metric (configs[4]: user x
 item MFMA scoring + train mask + top-20, d=256, 1M items) is reported under "scoring" in fp32 (the
-reference's precision, model.py:183; a 262,144-user batch so the f32-MFMA leg fits the run) and
-under "scoring_bf16" (SURVEY C5's bf16 inputs, 1M users): one step scores a fixed batch of query
+reference's precision, model.py:183) and under "scoring_bf16" (SURVEY C5's bf16 inputs), both on
+SURVEY C5's 1M query users: one step scores a fixed batch of query
 users against the full catalog, the batch split across ranks.
 
 value = K * nnz(A^) * steps / t  (edges/s), t = max over ranks of the barrier-bracketed loop.
@@ -441,6 +444,55 @@ def scoring_cpu_baseline(Q, items, pos, k, n_users):
                       f"top-{k} with the same train masks ({t:.1f}s); per-item rate extrapolated"}
 
 
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: run N ranks under
+    torch.distributed.run as CHILD processes (this process never touches the GPU: it is called
+    before any torch.cuda use, and it does not exec), forward rank 0's JSON line to stdout and
+    return non-zero if any rank failed or no line came back."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    print(f"[bench] launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    line = None
+    for raw in p.stdout:
+        s = raw.strip()
+        if s.startswith("{") and '"metric"' in s:
+            try:
+                json.loads(s)
+                line = s
+                continue
+            except ValueError:
+                pass
+        sys.stderr.write(raw)
+        sys.stderr.flush()
+    rc = p.wait()
+    if rc != 0 or line is None:
+        print(f"[bench] rank launch failed (exit {rc}, result line {'present' if line else 'missing'})",
+              file=sys.stderr, flush=True)
+        return rc if rc != 0 else 1
+    print(line, flush=True)
+    return 0
+
+
+def launch_check(args, world: int, rank: int) -> None:
+    """--launch-check: the rank-launch path without a GPU (CPU tests): join a gloo group, report it."""
+    if world > 1:
+        dist.init_process_group("gloo")
+    if os.environ.get("LGX_LAUNCH_CHECK_FAIL_RANK") == str(rank):  # tests: one rank dies
+        sys.exit(3)
+    pg = {"world_size": dist.get_world_size(), "backend": dist.get_backend()} if world > 1 else None
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "n_gpus": world, "process_group": pg}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -450,7 +502,7 @@ def main():
     ap.add_argument("--dtype", default="f32", choices=["bf16", "f32"],
                     help="storage dtype of the headline propagation run (f32 = the reference's, model.py:163-176)")
     ap.add_argument("--score-users", type=int, default=1_000_000, help="bf16 scoring leg users (configs[4])")
-    ap.add_argument("--score-f32-users", type=int, default=262_144, help="fp32 scoring leg users")
+    ap.add_argument("--score-f32-users", type=int, default=1_000_000, help="fp32 scoring leg users (configs[4])")
     ap.add_argument("--score-items", type=int, default=1_000_000)
     ap.add_argument("--score-steps", type=int, default=2)
     ap.add_argument("--cpu-nnz", type=int, default=40_000_000)
@@ -460,10 +512,21 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scoring", action="store_true")
     ap.add_argument("--no-propagation", action="store_true", help="development: scoring legs only")
+    ap.add_argument("--launch-check", action="store_true", help="tests: rank launch only, no GPU work")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no external launcher: start the N ranks here, before anything initialises the GPU
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        log(f"[bench] error: --gpus {args.gpus} but WORLD_SIZE={world}; the line would not be the "
+            f"{args.gpus}-GPU measurement")
+        sys.exit(2)
+    if args.launch_check:
+        launch_check(args, world, rank)
+        return
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     local_rank %= max(1, torch.cuda.device_count())  # identity on a real node; rehearsal ranks share a GPU
     torch.cuda.set_device(local_rank)
@@ -476,8 +539,6 @@ def main():
         else:
             dist.init_process_group(backend)
         log(f"[bench] world {dist.get_world_size()} over {dist.get_backend()}")
-    if world != args.gpus:
-        log(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}")
 
     def scoring_legs():
         if args.no_scoring:

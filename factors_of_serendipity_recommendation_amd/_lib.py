@@ -107,12 +107,15 @@ SIGNATURES = {
                                 _c_int, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "lgx_topk_rows": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _c_int, _vp, _vp, _vp]),
     "lgx_foldout_metrics": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _vp, _vp, _vp]),
+    "lgx_column_mean_f32": (_c_int, [_vp, _c_i64, _c_i64, _vp, _vp]),
     "lgx_gather_scores": (_c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp]),
     "lgx_synth_edges": (_c_int, [ctypes.c_uint64, _vp, _c_i64, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp]),
     "lgx_fill_normal": (_c_int, [_vp, _c_i64, ctypes.c_float, ctypes.c_uint64, _c_int, _vp]),
 }
 
 _lib = None
+# development A/B only (tools/*.py --lib): load an older build that lacks newer entry points
+ALLOW_MISSING = False
 
 
 def build(force: bool = False, jobs: int = 8) -> str:
@@ -134,6 +137,8 @@ def lib():
                 "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if ALLOW_MISSING and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -1184,11 +1184,14 @@ void score_topk_bf16_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf
         smem, a, xcd_affine, n_utiles, nbuf);
 }
 
-template <int KSTEPS, bool MINMAX, int MODE = 0>
-__global__ __launch_bounds__(kF32LdsWaves * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+// WAVES = 4: one wave per SIMD (d = 192, 256: the users' rows take 96-128 VGPRs).  WAVES = 8 (d <= 128,
+// whose rows take <= 64 VGPRs): two waves per SIMD in the bf16 walk's staggered order, so one wave's
+// top-k epilogue runs under its partner's MFMAs instead of between its own tiles.
+template <int KSTEPS, bool MINMAX, int MODE = 0, int WAVES = kF32LdsWaves>
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVES / 4, WAVES / 4)))
 void score_topk_f32_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    score_topk_lds_body<LGX_DTYPE_F32, KSTEPS, MINMAX, MODE, kF32LdsWaves, 2, false>(
+    score_topk_lds_body<LGX_DTYPE_F32, KSTEPS, MINMAX, MODE, WAVES, 2, (WAVES > 4)>(
         smem, a, xcd_affine, n_utiles, nbuf);
 }
 
@@ -1446,12 +1449,14 @@ int kch_for(int dtype, int64_t d) {
 struct StratThr {
     float t[32];
     int n;
-    float base, inv;  // estimate: floor((s - base) * inv) is the label within +-1 (thresholds ~ evenly spaced)
+    // estimate: floor(fma(s, inv, off)) is the label within +-1 (thresholds ~ evenly spaced; off =
+    // -base * inv, one FMA per score instead of a subtract and a multiply)
+    float base, inv, off;
 };
 
-// the label estimate of the kernel, on the host (same f32 operations, no contraction)
+// the label estimate of the kernel, on the host (the same single-rounding FMA as v_fma_f32)
 inline int strat_estimate(float sc, const StratThr& thr) {
-    const float x = (sc - thr.base) * thr.inv;
+    const float x = std::fmaf(sc, thr.inv, thr.off);
     return (x >= (float)thr.n || x != x) ? thr.n : (x < 0.0f ? 0 : (int)x);
 }
 inline int strat_label_host(float sc, const StratThr& thr) {
@@ -1562,7 +1567,7 @@ __global__ __launch_bounds__(kDenseWaves * 64) void strat_label_lds(const void* 
         }
     };
     auto label = [&](float sc) {
-        const float x = (sc - thr.base) * thr.inv;
+        const float x = __builtin_fmaf(sc, thr.inv, thr.off);
         int l = (int)__builtin_amdgcn_fmed3f(x, 0.0f, (float)thr.n);  // clamp to [0, n], then truncate
         if (x != x) l = thr.n;                                       // NaN -> n, as label_of
         if (EST1) {
@@ -1651,11 +1656,18 @@ struct SplitPlan {
 // doubles the barriers per MFMA, which costs more than the overlap of two independent workgroups
 // recovers.  f32: <4 waves, 64-item tiles>, one workgroup (one wave per SIMD) per CU.  Either way one
 // workgroup per CU, 256 resident.
-inline int lds_waves(int dtype) { return dtype == LGX_DTYPE_F32 ? kF32LdsWaves : kBf16LdsWaves; }
 inline int64_t lds_resident() { return 256; }
 
 constexpr size_t kLdsBytes = 160 * 1024;
 constexpr int kTileItems = 64;
+// fp32 LDS walk: 8 staggered waves (two per SIMD) where the users' rows leave the registers for it
+// (d <= 128) and two tiles fit beside 8 waves' lists, else 4 waves
+inline bool f32_lds8_fits(int64_t d, int k) {
+    return d <= 128 && 2 * (size_t)kTileItems * d * 4 + 8 * list_bytes_per_wave(k, lds_pend(true, (int)(d / 16))) <= kLdsBytes;
+}
+inline int lds_waves(int dtype, int64_t d, int k) {
+    return dtype == LGX_DTYPE_F32 ? (f32_lds8_fits(d, k) ? 8 : kF32LdsWaves) : kBf16LdsWaves;
+}
 // LDS kernel applies to bf16 with d a multiple of 32 up to 256 (even k-step counts are
 // instantiated) and to f32 with d a multiple of 64 up to 256, whenever two 64-item tiles fit beside
 // the top-k lists (8 waves with 12 deferred slots per lane / 4 waves with 4): d = 256 up to k = 20
@@ -1672,7 +1684,7 @@ bool lds_eligible(int dtype, int64_t d, int k) {
 SplitPlan plan_splits(int64_t B, int64_t n_items, int dtype, int64_t d, int k) {
     const int64_t tiles32 = ceil_div(n_items, 32);
     if (lds_eligible(dtype, d, k)) {
-        const int waves = lds_waves(dtype);
+        const int waves = lds_waves(dtype, d, k);
         const int64_t users = waves * kUsersPerWave, tile_items = kTileItems;
         const int64_t resident = lds_resident();
         const int64_t ut = ceil_div(B, users);
@@ -1764,21 +1776,21 @@ int launch_bf16_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t s
     return LGX_OK;
 }
 
-template <int KS, bool MM, int MODE>
+template <int KS, bool MM, int MODE, int WAVES = kF32LdsWaves>
 int launch_f32_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
-    typedef LdsGeom<KS, kF32LdsWaves, 2, 4> G;
-    const size_t lists = (size_t)kF32LdsWaves * list_bytes_per_wave(a.k, lds_pend(true, KS));
+    typedef LdsGeom<KS, WAVES, 2, 4> G;
+    const size_t lists = (size_t)WAVES * list_bytes_per_wave(a.k, lds_pend(true, KS));
     const int nbuf = lds_ring_buffers(G::TILE, lists, 1);
     const size_t shmem = (size_t)nbuf * G::TILE + lists;
     if (shmem > kLdsBytes) {
         set_error("lgx_score_topk: f32 LDS kernel needs %zu B of LDS", shmem);
         return LGX_ERR_UNSUPPORTED;
     }
-    int rc = set_lds_limit(score_topk_f32_lds<KS, MM, MODE>, shmem);
+    int rc = set_lds_limit(score_topk_f32_lds<KS, MM, MODE, WAVES>, shmem);
     if (rc) return rc;
     const unsigned grid = (unsigned)(p.n_utiles * p.n_splits);
-    score_topk_f32_lds<KS, MM, MODE><<<grid, kF32LdsWaves * 64, shmem, stream>>>(a, p.xcd_affine ? 1 : 0,
-                                                                                   p.n_utiles, nbuf);
+    score_topk_f32_lds<KS, MM, MODE, WAVES><<<grid, WAVES * 64, shmem, stream>>>(a, p.xcd_affine ? 1 : 0,
+                                                                                  p.n_utiles, nbuf);
     LGX_LAUNCH_CHECK();
     return LGX_OK;
 }
@@ -1794,6 +1806,15 @@ int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream, int d
     }
     if constexpr (MODE != kFloorOnly) {
         if (dtype == LGX_DTYPE_F32) {
+            if (p.waves == 8) {
+                switch (ksteps) {
+                    case 4: return launch_f32_lds_kernel<4, MM, MODE, 8>(a, p, stream);
+                    case 8: return launch_f32_lds_kernel<8, MM, MODE, 8>(a, p, stream);
+                    default:
+                        set_error("lgx_score_topk: no 8-wave f32 LDS kernel for d=%lld", (long long)a.d);
+                        return LGX_ERR_UNSUPPORTED;
+                }
+            }
             switch (ksteps) {
                 case 4: return launch_f32_lds_kernel<4, MM, MODE>(a, p, stream);
                 case 8: return launch_f32_lds_kernel<8, MM, MODE>(a, p, stream);
@@ -1925,7 +1946,8 @@ extern "C" int lgx_score_topk_plan(int64_t B, int64_t n_items, int64_t d, int dt
     size_t off = 0;
     for (int i = 0; i < n && off < len; ++i) {
         const SplitPlan& p = r[i].p;
-        const char* kern = p.lds ? (dtype == LGX_DTYPE_F32 ? "score_topk_f32_lds<4 waves, 64-item tiles, 16x16x4>"
+        const char* kern = p.lds ? (dtype == LGX_DTYPE_F32 ? (p.waves == 8 ? "score_topk_f32_lds<8 waves, 64-item tiles, 16x16x4>"
+                                                                            : "score_topk_f32_lds<4 waves, 64-item tiles, 16x16x4>")
                                                            : "score_topk_bf16_lds<8 waves, 64-item tiles, 16x16x32>")
                                  : (v1_waves(k) == 4 ? "score_topk_kernel<4 waves>" : "score_topk_kernel<1 wave>");
         const char* mode = p.lds ? (p.n_splits == 1 ? "full-sweep" : (p.xcd_affine ? "split-xcd" : "split"))
@@ -2143,6 +2165,7 @@ extern "C" int lgx_strat_labels_fused(const void* Q, const int64_t* user_rows, c
                                ? (thr.t[num_fold - 1] - thr.t[0]) / (num_fold - 1) : inter16);
     thr.inv = num_fold > 1 && std::isfinite(thr.t[num_fold - 1]) && thr.t[num_fold - 1] > thr.t[0]
                   ? (float)(num_fold - 1) / (thr.t[num_fold - 1] - thr.t[0]) : 1.0f / inter16;
+    thr.off = -(thr.base * thr.inv);  // any value serves: the host proof below runs the same FMA
     if (B == 0 || n_items == 0) return LGX_OK;
     const int64_t n_ug = ceil_div(B, (int64_t)kDenseUsers);
     const int64_t tiles = ceil_div(n_items, 32);

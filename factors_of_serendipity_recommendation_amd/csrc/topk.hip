@@ -229,6 +229,28 @@ __global__ __launch_bounds__(kFoldUsers) void foldout_staged_kernel(const int32_
     for (int i = t; i < nu * W; i += kFoldUsers) results[u0 * W + i] = oimg[(i / W) * S + i % W];
 }
 
+// np.mean(a, axis=0) of a C-contiguous float32 [rows, cols] array, as numpy computes it: per column a
+// float32 sum over the rows in row order (numpy's axis-0 add.reduce adds whole rows, no pairwise
+// blocking), then one float32 division by the row count.  One lane per column, so a row step is one
+// coalesced read per wave; the loads run ahead of the dependent adds.
+__global__ __launch_bounds__(64) void column_mean_kernel(const float* __restrict__ src, int64_t rows, int64_t cols,
+                                                        float* __restrict__ out) {
+    const int64_t j = blockIdx.x * (int64_t)64 + threadIdx.x;
+    if (j >= cols) return;
+    const float* p = src + j;
+    float acc = 0.0f;
+    int64_t i = 0;
+    for (; i + 8 <= rows; i += 8) {
+        float v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = p[(i + q) * cols];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc = acc + v[q];
+    }
+    for (; i < rows; ++i) acc = acc + p[i * cols];
+    out[j] = rows > 0 ? acc / (float)rows : NAN;
+}
+
 template <int R>
 int launch_topk_rows(const float* S, int64_t rows, int64_t cols, int64_t ld, int k, int32_t* out_idx,
                      float* out_val, bool vec, hipStream_t st) {
@@ -277,6 +299,17 @@ extern "C" int lgx_foldout_metrics(const int32_t* rankings, int64_t users, int k
         foldout_kernel<<<ceil_div(users, 128), 128, 0, as_hip(stream)>>>(rankings, users, k, truth_indptr,
                                                                           truth_indices, inv_log2, results);
     }
+    LGX_LAUNCH_CHECK();
+    return LGX_OK;
+}
+
+extern "C" int lgx_column_mean_f32(const float* src, int64_t rows, int64_t cols, float* out, lgx_stream_t stream) {
+    LGX_REQUIRE(rows >= 0 && cols >= 0 && (cols == 0 || out) && (rows == 0 || cols == 0 || src), LGX_ERR_INVALID_ARG,
+                "lgx_column_mean_f32: bad arguments");
+    LGX_REQUIRE(rows < (1LL << 24), LGX_ERR_UNSUPPORTED,
+                "lgx_column_mean_f32: %lld rows (the float32 row count is exact below 2^24)", (long long)rows);
+    if (cols == 0) return LGX_OK;
+    column_mean_kernel<<<(unsigned)ceil_div(cols, (int64_t)64), 64, 0, as_hip(stream)>>>(src, rows, cols, out);
     LGX_LAUNCH_CHECK();
     return LGX_OK;
 }

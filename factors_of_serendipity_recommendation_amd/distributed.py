@@ -176,7 +176,7 @@ def pad_table(full: torch.Tensor, bounds: np.ndarray, pad: int) -> torch.Tensor:
     return out
 
 
-def _row_gather(G: CSRGraph, rows: torch.Tensor, seg_len: Optional[int]) -> CSRGraph:
+def _row_gather(G: CSRGraph, rows: torch.Tensor) -> CSRGraph:
     """The rows `rows` of G, in that order, as a CSR (columns keep their order within each row)."""
     dev = G.indptr.device
     rows = rows.to(device=dev, dtype=torch.int64)
@@ -200,7 +200,7 @@ def chunk_push_operator(A_push: CSRGraph, world: int, mi: int, n_chunks: int) ->
     for c0 in range(0, mi, mc):
         m = min(mc, mi - c0)
         rows = (torch.arange(world, dtype=torch.int64)[:, None] * mi + c0 + torch.arange(m)[None, :]).reshape(-1)
-        G = _row_gather(A_push, rows.to(dev), seg_len)
+        G = _row_gather(A_push, rows.to(dev))
         G.plan = make_plan(G.indptr.cpu().numpy(), seg_len)
         G.ensure_plan()
         out.append((G, c0, m))
@@ -209,12 +209,17 @@ def chunk_push_operator(A_push: CSRGraph, world: int, mi: int, n_chunks: int) ->
 
 class PhaseRecorder:
     """Per-step stamps on the compute stream (HIP events; host clock for CPU tensors): the time
-    between two stamps is charged to the label of the later one."""
+    between two stamps is charged to the label of the later one.  At most `keep` steps hold their
+    events; older ones are folded into running totals (waiting for their last event, which is long
+    done by then), so a recorder left on through a training run stays bounded."""
 
-    def __init__(self, cuda: bool):
+    def __init__(self, cuda: bool, keep: int = 32):
         self.cuda = cuda
+        self.keep = keep
         self.steps: List[List[Tuple[str, object]]] = []
         self._cur: Optional[List[Tuple[str, object]]] = None
+        self._tot: Dict[str, float] = {}
+        self._n = 0
 
     def _stamp(self):
         if self.cuda:
@@ -234,16 +239,24 @@ class PhaseRecorder:
         if self._cur is not None:
             self.steps.append(self._cur)
             self._cur = None
+            while len(self.steps) > self.keep:
+                self._fold(self.steps.pop(0))
+
+    def _fold(self, st) -> None:
+        if self.cuda:
+            st[-1][1].synchronize()
+        for (_, a), (label, b) in zip(st[:-1], st[1:]):
+            dt = a.elapsed_time(b) if self.cuda else (b - a) * 1e3
+            self._tot[label] = self._tot.get(label, 0.0) + dt
+        self._n += 1
 
     def summary(self) -> Dict[str, float]:
         """Mean milliseconds per step by label (call after the stream has drained)."""
-        tot: Dict[str, float] = {}
         for st in self.steps:
-            for (_, a), (label, b) in zip(st[:-1], st[1:]):
-                dt = a.elapsed_time(b) if self.cuda else (b - a) * 1e3
-                tot[label] = tot.get(label, 0.0) + dt
-        n = max(1, len(self.steps))
-        return {k: v / n for k, v in tot.items()}
+            self._fold(st)
+        self.steps = []
+        n = max(1, self._n)
+        return {k: v / n for k, v in self._tot.items()}
 
 
 LayerFn = Callable[..., None]
@@ -293,7 +306,9 @@ class ShardedPropagation:
         so that a one-GPU RCCL group runs the async collective stream ordering the overlap depends on.
 
         n_chunks: push launches per layer (default 4 with collectives, else 1), each followed by its
-        own all-to-all.  sum_fn(src [n, rows, d], out [rows, d]): the ordered slab sum (default
+        own all-to-all.  The chunk operators hold copies of the push rows (C4 / 8: ~1 GB per rank
+        beside shard.A_push); a caller that keeps no other use for shard.A_push may drop it after
+        construction (self.push_nnz keeps its count).  sum_fn(src [n, rows, d], out [rows, d]): the ordered slab sum (default
         lgx_sum_slabs on the GPU, the same left-to-right adds on the host)."""
         self.s = shard
         self.K = K
@@ -327,6 +342,7 @@ class ShardedPropagation:
             n_chunks = 4 if self._collective else 1
         self.push_chunks = chunk_push_operator(s.A_push, s.world, s.mi, n_chunks) if n_chunks > 1 else \
             [(s.A_push, 0, s.mi)]
+        self.push_nnz = sum(c[0].nnz for c in self.push_chunks)
         self.R = torch.zeros_like(self.P)  # received partials: chunk c = [world, mc_c, d] slabs
         self.sum_fn = sum_fn or (_default_sum_fn if dev.type == "cuda" else _host_sum)
         self.record_phases = False

@@ -99,12 +99,42 @@ def _metrics(r: np.ndarray, recall_n: np.ndarray, topks: Sequence[int]) -> Dict:
     return {"recall": np.array(rec), "precision": np.array(pre), "ndcg": np.array(ndcg)}
 
 
+def _fingerprint(lists, keys) -> tuple:
+    """A cheap content check of a dict / sequence of lists at a few fixed keys: (length, first, last)
+    of each sampled list.  Catches a list edited in place (same dict object, same length) without
+    walking the whole dict on every call."""
+    out = []
+    for u in keys:
+        v = lists[u]
+        n = len(v)
+        out.append((n, int(v[0]) if n else -1, int(v[-1]) if n else -1))
+    return tuple(out)
+
+
+def _sample_keys(seq, n: int = 32) -> list:
+    """Up to n evenly spaced entries of seq (always its first and last)."""
+    if len(seq) <= n:
+        return list(seq)
+    return [seq[int(i)] for i in np.linspace(0, len(seq) - 1, n).round().astype(np.int64)]
+
+
+def clear_caches() -> None:
+    """Drop the device lists Test / batch_test keep between calls (and the dicts they hold).  Call it
+    after changing testDict, train_items, test_set or a dataset's positives in a way the built-in
+    check (same objects, same lengths, the same lists at 32 sampled users) cannot see, or to free
+    the device memory once evaluation is over."""
+    _TestLists._cache.clear()
+    _BatchLists._cache.clear()
+
+
 class _TestLists:
     """The static lists of one evaluation set on the device: the test users (row ids), their train
     positives (the mask CSR) and their test items as sorted (row * M + item) keys.  Procedure.Test
     runs every few epochs over the same testDict / allPos; building these from Python lists was most
     of its time (profiles/r04_rows.json, a7 phases), so they are kept for as long as the same
-    testDict object is passed (the reference never mutates it after loading, dataloader.py:282-293)."""
+    testDict object is passed (the reference never mutates it after loading, dataloader.py:282-293)
+    and the lists of 32 sampled users, test items and positives, still read the same (_fingerprint);
+    clear_caches() drops them."""
 
     _cache: Dict[tuple, "_TestLists"] = {}
 
@@ -114,6 +144,8 @@ class _TestLists:
         n = len(self.users)
         self.rows = torch.as_tensor(self.users, dtype=torch.int64, device=dev)
         self.mask = ops.lists_to_device_csr(dataset.getUserPosItems(self.users), dev, sort=True)
+        self.probe = _sample_keys(self.users)
+        self.stamp = self.fingerprint(dataset)
         truths = [testDict[u] for u in self.users]
         self.recall_n = np.fromiter(map(len, truths), dtype=np.int64, count=n)
         self.recall_n_dev = torch.from_numpy(self.recall_n).to(dev)
@@ -122,12 +154,19 @@ class _TestLists:
         keys = np.repeat(np.arange(n, dtype=np.int64), self.recall_n) * self.M + flat
         self.keys = torch.unique(torch.from_numpy(keys).to(dev))  # sorted
 
+    def fingerprint(self, dataset) -> tuple:
+        try:
+            return (_fingerprint(self.testDict, self.probe),
+                    _fingerprint(list(dataset.getUserPosItems(self.probe)), range(len(self.probe))))
+        except (KeyError, IndexError):
+            return ()
+
     @classmethod
     def get(cls, dataset, n_items: int, dev) -> "_TestLists":
         td = dataset.testDict
         key = (id(dataset), id(td), len(td), n_items, str(dev))
         hit = cls._cache.get(key)
-        if hit is None or hit.testDict is not td:
+        if hit is None or hit.testDict is not td or hit.fingerprint(dataset) != hit.stamp:
             cls._cache.clear()
             hit = cls._cache[key] = cls(dataset, td, n_items, dev)
         return hit
@@ -168,13 +207,16 @@ class _BatchLists:
     """batch_test's per-user lists on the device: row ids, the train-item mask (flag 0) and the
     truth lists, built once for a given (users, train_items, test_set, flag) and reused while the
     same dict objects and the same users come back (the reference's data_generator holds them for
-    the whole run, batch_test.py:12-23)."""
+    the whole run, batch_test.py:12-23) and the lists of 32 sampled users still read the same;
+    clear_caches() drops them."""
 
     _cache: Dict[tuple, "_BatchLists"] = {}
 
     def __init__(self, users: np.ndarray, train_items, test_set, flag: int, dev):
         self.train_items, self.test_set, self.users = train_items, test_set, users  # held (ids stay valid)
         ul = users.tolist()
+        self.probe = _sample_keys(ul)
+        self.stamp = self.fingerprint()
         self.rows = torch.as_tensor(users, dtype=torch.int64, device=dev)
         if flag == 0:
             truths = [test_set[u] for u in ul]
@@ -184,13 +226,20 @@ class _BatchLists:
             self.mask = None
         self.truth = ops.lists_to_device_csr(truths, dev, sort=False)
 
+    def fingerprint(self) -> tuple:
+        try:
+            return (_fingerprint(self.train_items, self.probe),
+                    _fingerprint(self.test_set, self.probe) if self.test_set is not None else ())
+        except (KeyError, IndexError, TypeError):
+            return ()
+
     @classmethod
     def get(cls, users_to_test, train_items, test_set, flag: int, dev) -> "_BatchLists":
         users = np.fromiter((int(u) for u in users_to_test), dtype=np.int64)
         key = (id(train_items), id(test_set), len(users), flag, str(dev))
         hit = cls._cache.get(key)
         if (hit is None or hit.train_items is not train_items or hit.test_set is not test_set
-                or not np.array_equal(hit.users, users)):
+                or not np.array_equal(hit.users, users) or hit.fingerprint() != hit.stamp):
             cls._cache.clear()
             hit = cls._cache[key] = cls(users, train_items, test_set, flag, dev)
         return hit
@@ -201,15 +250,16 @@ def batch_test(user_emb: torch.Tensor, item_emb: torch.Tensor, users_to_test: Se
                Ks: Sequence[int] = (20,), train_set_flag: int = 0) -> Dict:
     """batch_test.test (batch_test.py:25-84): raw dot-product ratings, training items set to -inf
     and the test set as truth (train_set_flag=0, :57-65), or no mask and the train items as truth
-    (train_set_flag=1, :66-68); top-max(Ks), fold-out curves, float32 mean over users."""
+    (train_set_flag=1, :66-68); top-max(Ks), fold-out curves, and their mean over users as the
+    reference's np.mean(all_result, axis=0) computes it (:75-76: float32 sums in user order, one float32
+    division), on the device bit for bit (lgx_column_mean_f32)."""
     top_show = np.sort(np.asarray(Ks))
     max_top = int(max(top_show))
     bl = _BatchLists.get(users_to_test, train_items, test_set, train_set_flag, user_emb.device)
     idx, _ = ops.score_topk(user_emb, item_emb, max_top, user_rows=bl.rows, mask=bl.mask, mask_value=float("-inf"))
     curves = ops.foldout_metrics(idx, bl.truth)
-    # the users' mean on the device (summed in float64, rounded to float32 once): only 5 x max_top
-    # values cross to the host
-    mean = (curves.double().sum(0) / max(1, curves.shape[0])).float().cpu().numpy()
+    # the users' mean on the device: only 5 x max_top values cross to the host
+    mean = ops.column_mean(curves).cpu().numpy()
     final = mean.reshape(5, max_top)[:, top_show - 1].reshape(5, len(top_show))
     return {"precision": final[0].astype(np.float64), "recall": final[1].astype(np.float64),
             "ndcg": final[3].astype(np.float64)}

@@ -311,6 +311,19 @@ def foldout_metrics(rankings: torch.Tensor, truth: Tuple[torch.Tensor, torch.Ten
     return out
 
 
+def column_mean(x: torch.Tensor) -> torch.Tensor:
+    """np.mean(x, axis=0) of a float32 [rows, cols] matrix, bit for bit (batch_test.py:75-76): float32
+    sums in row order, one float32 division by rows (lgx_column_mean_f32) -> f32 [cols]."""
+    require_gpu(x)
+    if x.dtype != torch.float32 or x.dim() != 2:
+        raise ValueError("column_mean: float32 [rows, cols] expected")
+    x = x.contiguous()
+    out = torch.empty(x.shape[1], dtype=torch.float32, device=x.device)
+    _lib.check(_lib.lib().lgx_column_mean_f32(x.data_ptr(), x.shape[0], x.shape[1], out.data_ptr(),
+                                              _stream_ptr(x.device)), "lgx_column_mean_f32")
+    return out
+
+
 def gather_scores(emb_user: torch.Tensor, emb_item: torch.Tensor, cand: Tuple[torch.Tensor, torch.Tensor],
                   n_pairs: int) -> torch.Tensor:
     """Per-user candidate dots (recommend.py:167-171, :214-217) -> f32 [n_pairs].  List u is scored

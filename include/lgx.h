@@ -267,6 +267,14 @@ int lgx_topk_rows(const float* S, int64_t rows, int64_t cols, int64_t ld, int k,
 int lgx_foldout_metrics(const int32_t* rankings, int64_t users, int k, const int64_t* truth_indptr,
                         const int32_t* truth_indices, const double* inv_log2, float* results,
                         lgx_stream_t stream);
+/*
+ * batch_test's users' mean of the fold-out curves (LightGCN-tf/utility/batch_test.py:75-76,
+ * np.mean(all_result, axis=0) over a float32 [rows, cols] array): out[j] = the float32 sum of
+ * src[0][j], src[1][j], ... in row order, divided once in float32 by rows -- numpy's result bit for bit
+ * (its axis-0 reduction adds whole rows, it does not block pairwise).  src C-contiguous, rows < 2^24;
+ * rows = 0 gives NaN as np.mean of an empty axis does.
+ */
+int lgx_column_mean_f32(const float* src, int64_t rows, int64_t cols, float* out, lgx_stream_t stream);
 
 /* ---------------------------------------------------------------- a11/a12: candidate similarity */
 /*

@@ -1,5 +1,6 @@
-"""CPU: the N>1 propagation schedule (user shards; items by push + reduce-scatter, users by pull
-from the all-gathered item table) over a gloo process group, world sizes 2 and 3, against the
+"""CPU: the N>1 propagation schedule (user shards; items by a chunked push whose partials are
+exchanged per chunk and summed in rank order, users by pull from the all-gathered item table)
+over a gloo process group, world sizes 2, 3, 4 and 8, against the
 float64 oracle.  The SpMM and epilogue callables are the oracle (injected); the orchestration,
 operators, padding and collectives are the product code of distributed.py."""
 import os

@@ -1,7 +1,7 @@
 """GPU: the multi-GPU propagation schedule with the REAL HIP layer kernels.  The box has one GPU,
 so the two ranks share cuda:0 and exchange over gloo (RCCL refuses two ranks on one device); a
-world-1 RCCL group with the collectives forced on runs the async reduce-scatter / all-gather
-stream ordering on the device; the 8-GPU RCCL run is the bench's job.  Checked against the
+world-1 RCCL group with the collectives forced on runs the chunked push's async all-to-alls
+(summed in rank order by lgx_sum_slabs) and the item all-gather on the device; the 8-GPU RCCL run is the bench's job.  Checked against the
 float64 oracle (fp32 tolerance)."""
 import os
 import socket
@@ -96,8 +96,8 @@ def test_sharded_propagation_real_kernels(world, K, dt):
 
 @pytest.mark.parametrize("K,dt", [(3, "f32"), (3, "bf16")])
 def test_sharded_propagation_world1_rccl_forced_collectives(K, dt):
-    """One rank, backend "nccl" (RCCL): the reduce-scatter and all-gather are issued as async RCCL
-    collectives on their own stream (the world>1 code path), not the world-1 copies."""
+    """One rank, backend "nccl" (RCCL): the push chunks' all-to-alls and the item all-gather are
+    issued as async RCCL collectives (the world>1 code path), not the world-1 copies."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_worker, args=(0, 1, _free_port(), K, dt, q, "nccl"))

@@ -647,28 +647,35 @@ def test_similarity_minmax():
     assert abs(mn - omn) <= 1e-5 * abs(omn) and abs(mx - omx) <= 1e-5 * abs(omx)
 
 
-@pytest.mark.parametrize("flag", [0, 1])
-def test_batch_test_both_flags_vs_oracle(mlls, flag):
+@pytest.mark.parametrize("flag,Ks,d", [(0, [50, 20, 5], 64), (1, [50, 20, 5], 64), (0, [20, 5], 64),
+                                       (1, [20, 5], 64), (0, [20, 5], 128), (1, [20, 5], 128)])
+def test_batch_test_both_flags_vs_oracle(mlls, flag, Ks, d):
     """evaluator.batch_test == oracle.batch_test (batch_test.py:25-84) on the mlls KAT inputs, with
     train_set_flag 0 (mask train, truth = test) and 1 (no mask, truth = train items, :66-68), Ks
-    unsorted as the reference allows; over 2 of its 1024-user batches' worth of repeated users."""
+    unsorted as the reference allows; over 2 of its 1024-user batches' worth of repeated users.
+    max(Ks) = 50 runs the register-fragment kernel, 20 the fp32 LDS walk (8 staggered waves); d = 128
+    uses random embeddings on the same graph."""
     U, I = int(mlls["n_users"]), int(mlls["n_items"])
     A = lgx.build_norm_adj(mlls["train_users"], mlls["train_items"], U, I, dedup=True, device=DEV)
-    E0 = torch.from_numpy(np.concatenate([mlls["emb_user"], mlls["emb_item"]])).to(DEV)
+    if d == 64:
+        E0 = torch.from_numpy(np.concatenate([mlls["emb_user"], mlls["emb_item"]])).to(DEV)
+    else:
+        E0 = torch.from_numpy((np.random.default_rng(7).standard_normal((U + I, d)) * 0.1).astype(np.float32)).to(DEV)
+    assert ops.score_topk_plan(3 * len(mlls["test_users"]), I, d, torch.float32, max(Ks)).startswith(
+        "score_topk_f32_lds<8 waves") == (max(Ks) <= 32)
     out = lgx.propagate(A, E0, 4)
     tp, tx = mlls["train_list_indptr"], mlls["train_list_indices"]
     train = {int(u): list(tx[tp[j]:tp[j + 1]]) for j, u in enumerate(mlls["train_list_users"])}
     sp_, sx = mlls["test_indptr"], mlls["test_indices"]
     test = {int(u): list(sx[sp_[j]:sp_[j + 1]]) for j, u in enumerate(mlls["test_users"])}
     users = [int(u) for u in mlls["test_users"]] * 3
-    Ks = [50, 20, 5]
     got = evaluator.batch_test(out[:U], out[U:], users, train, test, Ks=Ks, train_set_flag=flag)
     o = out.cpu().numpy()
     ref = oracle.batch_test(o[:U], o[U:], users, train, test, Ks=Ks, train_set_flag=flag)
     for key in ("precision", "recall", "ndcg"):
         # the GPU f32 scores vs the oracle's f64-rounded ones can swap a near-tie (SURVEY 8(a)(ii))
         assert np.allclose(got[key], ref[key], rtol=0, atol=2e-4), (key, got[key], ref[key])
-    if flag == 1:
+    if flag == 1 and d == 64:
         assert got["precision"][0] > 0.3  # the train items rank first without a mask
 
 
@@ -711,3 +718,17 @@ def test_a_split_folds_into_lightgcn(mlls, tmp_path):
         ua, ia = a.computer()
         ub, ib = b.computer()
     assert torch.equal(ua, ub) and torch.equal(ia, ib)
+
+
+@pytest.mark.parametrize("rows,cols", [(27522, 100), (1, 5), (52643, 500), (0, 7)])
+def test_column_mean_is_numpy_mean_bit_for_bit(rows, cols):
+    """lgx_column_mean_f32 == np.mean(a, axis=0) of float32 (batch_test.py:75-76), bit for bit."""
+    a = (np.random.default_rng(rows + cols).random((rows, cols)) * 0.3).astype(np.float32)
+    got = ops.column_mean(torch.from_numpy(a).to(DEV)).cpu().numpy()
+    with np.errstate(invalid="ignore", divide="ignore"):
+        import warnings
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            want = np.mean(a, axis=0)
+    assert want.dtype == np.float32
+    assert np.array_equal(got, want, equal_nan=True)

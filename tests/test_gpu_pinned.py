@@ -382,17 +382,18 @@ def test_c5_full_catalog_1m_items_bench_plan():
 def test_c5_fp32_scoring_leg_plan_and_values():
     """The fp32 scoring leg of the bench (the reference's precision, model.py:183, Procedure.py:127-135)
     on the bench's own launch plan: f32 query and item tables through score_topk_f32_lds (16x16x4 f32
-    MFMA, 4 waves x 32 users per workgroup), 32,768 users = 256 user tiles = one full round of the
-    256 resident workgroups, x 1,000,000 items, d=256, top-20, 50 masked items per user.  The plan
-    equals the bench's 262,144-user plan launch for launch -- one full sweep seeded in stages (7
-    launches over [0,16384), ..., [524288, 1M)), "seeded" included in the comparison -- and 1,500
-    users spread over every workgroup are checked against float64 scores."""
-    B, I, d, k = 32768, 1_000_000, 256, 20
+    MFMA, 4 waves x 32 users per workgroup at d=256), x 1,000,000 items, d=256, top-20, 50 masked
+    items per user.  The bench scores SURVEY C5's 1,000,000 users: 7,813 user tiles = 30 full rounds of
+    the 256 resident workgroups (one full sweep seeded in stages: 7 launches over [0,16384), ...,
+    [524288, 1M)) plus a 133-tile partial round, launched catalog-split.  Here 256 + 133 tiles
+    (49,792 users) give the same plan launch for launch ("seeded" and n_splits included), and 1,500
+    users spread over every workgroup of both launches are checked against float64 scores."""
+    B, I, d, k = 128 * (256 + 133), 1_000_000, 256, 20
     plan = ops.score_topk_plan(B, I, d, torch.float32, k)
-    bench = ops.score_topk_plan(262144, I, d, torch.float32, k)
+    bench = ops.score_topk_plan(1_000_000, I, d, torch.float32, k)
     assert _plan_kinds(plan) == _plan_kinds(bench), (plan, bench)
-    assert len(_plan_kinds(plan)) == 1 and plan.startswith("score_topk_f32_lds"), plan
-    assert "full-sweep (seeded in stages)" in plan, plan
+    assert len(_plan_kinds(plan)) == 2 and plan.startswith("score_topk_f32_lds<4 waves"), plan
+    assert "full-sweep (seeded in stages)" in plan and "split" in plan.split("; ")[1], plan
     g = torch.Generator(device=DEV).manual_seed(57)
     Q = torch.randn(B, d, device=DEV, generator=g) / 16
     items = torch.randn(I, d, device=DEV, generator=g) / 16
@@ -404,7 +405,8 @@ def test_c5_fp32_scoring_leg_plan_and_values():
     mask = (indptr, m[keep].to(torch.int32))
     idx, val = lgx.score_topk(Q, items, k, mask=mask)
     # every 128-user workgroup, and every wave lane position, is sampled
-    sel = torch.cat([torch.arange(0, B, 128, device=DEV) + torch.randint(0, 128, (B // 128,), device=DEV, generator=g),
-                     torch.randint(0, B, (1500 - B // 128,), device=DEV, generator=g)])
+    nt = B // 128
+    sel = torch.cat([torch.arange(0, B, 128, device=DEV) + torch.randint(0, 128, (nt,), device=DEV, generator=g),
+                     torch.randint(0, B, (1500 - nt,), device=DEV, generator=g)])
     assert sel.numel() == 1500
     _masked_topk_check(Q, items, idx, val, mask, sel, k)

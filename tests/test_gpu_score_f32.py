@@ -1,7 +1,8 @@
 """GPU: the fp32 scoring path (the reference's precision: model.py:183 fp32 matmul + Procedure.py:
 134-135 mask and torch.topk) through score_topk_f32_lds -- the LDS-ring walk on
-v_mfma_f32_16x16x4_f32 -- in every launch mode the planner uses: catalog split (small batches),
-full sweep (>= 256 user tiles of 128), full sweep seeded in stages (>= 262 144 items), the split tail
+v_mfma_f32_16x16x4_f32, 4 waves x 32 users (d > 128) or 8 staggered waves x 32 users (d <= 128) --
+in every launch mode the planner uses: catalog split (small batches), full sweep (>= 256 user
+tiles), full sweep seeded in stages (>= 262 144 items), the split tail
 of a partial last round, user_rows, the min / max variant; and the fall-back kernel where the LDS
 budget rules the walk out (d = 256 with k > 20).  Checked on the device against float64 scores:
 k distinct unmasked items, each within 1e-5 of the exact k-th best, values = the float64 scores to
@@ -47,11 +48,14 @@ def _check(Q, items, idx, val, mask, sel, k, user_rows=None, chunk=250):
         assert torch.allclose(val[s].double(), got, rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("d,k,lds", [(64, 20, True), (128, 32, True), (192, 7, True), (256, 20, True),
-                                     (256, 21, False), (96, 20, False), (32, 20, False)])
-def test_f32_kernel_selection(d, k, lds):
+@pytest.mark.parametrize("d,k,lds,waves", [(64, 20, True, 8), (128, 20, True, 8), (128, 32, True, 4),
+                                           (192, 7, True, 4), (256, 20, True, 4), (256, 21, False, 0),
+                                           (96, 20, False, 0), (32, 20, False, 0)])
+def test_f32_kernel_selection(d, k, lds, waves):
     plan = ops.score_topk_plan(40_000, 100_000, d, torch.float32, k)
     assert plan.startswith("score_topk_f32_lds") == lds, plan
+    if lds:
+        assert plan.startswith(f"score_topk_f32_lds<{waves} waves"), plan
 
 
 @pytest.mark.parametrize("B,I,d,k,per", [(1000, 50_000, 64, 20, 30), (3000, 20_011, 256, 20, 50),
@@ -67,29 +71,32 @@ def test_f32_split_mode(B, I, d, k, per):
     _check(Q, items, idx, val, mask, torch.arange(0, B, max(1, B // 600), device=DEV), k)
 
 
-def test_f32_full_sweep_with_split_tail_and_user_rows():
-    """256 full user tiles of 128 plus a 40-tile partial round (its own split launch), user_rows
-    permuting a larger query table, masked."""
-    B, I, d, k = 128 * (256 + 40), 30_000, 256, 20
+@pytest.mark.parametrize("d,waves", [(256, 4), (128, 8), (64, 8)])
+def test_f32_full_sweep_with_split_tail_and_user_rows(d, waves):
+    """256 full user tiles plus a 40-tile partial round (its own split launch), user_rows permuting a
+    larger query table, masked: the 4-wave walk (d = 256, 128-user tiles) and the staggered 8-wave
+    walk (d <= 128, 256-user tiles)."""
+    B, I, k = 32 * waves * (256 + 40), 30_000, 20
     plan = ops.score_topk_plan(B, I, d, torch.float32, k)
-    assert "full-sweep" in plan and plan.count("score_topk_f32_lds") == 2, plan
+    assert "full-sweep" in plan and plan.count(f"score_topk_f32_lds<{waves} waves") == 2, plan
     g = torch.Generator(device=DEV).manual_seed(3)
     Q = torch.randn(B + 500, d, device=DEV, generator=g) / 8
     items = torch.randn(I, d, device=DEV, generator=g) / 8
     rows = torch.randperm(B + 500, device=DEV, generator=g)[:B]
     mask = _mask(B, I, 50, g)
     idx, val = lgx.score_topk(Q, items, k, user_rows=rows, mask=mask)
-    sel = torch.cat([torch.randint(0, 128 * 256, (600,), device=DEV, generator=g),
-                     torch.randint(128 * 256, B, (600,), device=DEV, generator=g)])
+    full = 32 * waves * 256
+    sel = torch.cat([torch.randint(0, full, (600,), device=DEV, generator=g),
+                     torch.randint(full, B, (600,), device=DEV, generator=g)])
     _check(Q, items, idx, val, mask, sel, k, user_rows=rows)
 
 
 def test_f32_seeded_stages_equal_one_sweep_and_float64():
     """>= 262 144 items: the sweep runs in seeded stages; the lists equal (as sets) the unseeded
     one-launch min / max variant and the float64 top-k; min / max equal the float64 extremes."""
-    B, I, d, k = 128 * 256, 300_000, 128, 20
+    B, I, d, k = 256 * 256, 300_000, 128, 20
     plan = ops.score_topk_plan(B, I, d, torch.float32, k)
-    assert "full-sweep (seeded in stages)" in plan and plan.startswith("score_topk_f32_lds"), plan
+    assert "full-sweep (seeded in stages)" in plan and plan.startswith("score_topk_f32_lds<8 waves"), plan
     g = torch.Generator(device=DEV).manual_seed(5)
     Q = torch.randn(B, d, device=DEV, generator=g) / 8
     items = torch.randn(I, d, device=DEV, generator=g) / 8

@@ -128,14 +128,23 @@ def _mlls_loader(mlls, tmp_path):
     return Loader(path=str(tmp_path), device=DEV)
 
 
-def test_procedure_test_matches_oracle_restatement(mlls, tmp_path):
+@pytest.mark.parametrize("topks,d", [([20, 100], 64), ([20], 64), ([5, 20], 128)])
+def test_procedure_test_matches_oracle_restatement(mlls, tmp_path, topks, d):
+    """evaluator.Test == Procedure.Test restated by the oracle on the mlls graph: the shipped d = 64
+    embeddings at k = 100 (the register-fragment kernel) and k = 20 (the fp32 LDS walk, 8 staggered
+    waves, catalog split), and random d = 128 embeddings at k = 20 (the same walk at d = 128)."""
     from factors_of_serendipity_recommendation_amd.model import LightGCN
     ds = _mlls_loader(mlls, tmp_path)
     eu, ei = mlls["emb_user"].astype(np.float32), mlls["emb_item"].astype(np.float32)
+    if d != eu.shape[1]:
+        rng = np.random.default_rng(d)
+        eu = (rng.standard_normal((eu.shape[0], d)) * 0.1).astype(np.float32)
+        ei = (rng.standard_normal((ei.shape[0], d)) * 0.1).astype(np.float32)
+    plan = ops.score_topk_plan(len(ds.testDict), ei.shape[0], d, torch.float32, max(topks))
+    assert plan.startswith("score_topk_f32_lds<8 waves") == (max(topks) <= 32), plan
     cfg = {"latent_dim_rec": eu.shape[1], "lightGCN_n_layers": 3, "keep_prob": 0.6, "A_split": False,
            "pretrain": 1, "user_emb": eu, "item_emb": ei, "dropout": 0}
     model = LightGCN(cfg, ds).to(DEV)
-    topks = [20, 100]
     got = evaluator.Test(ds, model, topks=topks)
 
     # oracle: Procedure.Test restated on the CPU (f64 propagation of the same adjacency)

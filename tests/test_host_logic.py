@@ -360,3 +360,42 @@ def test_batch_lists_cache_reuse_and_invalidation():
     f1 = evaluator._BatchLists.get(users, train, test, 1, dev)
     tp, tx = f1.truth
     assert f1.mask is None and tx[tp[0]:tp[1]].tolist() == train[users[0]]
+
+
+def test_eval_caches_see_in_place_edits_and_clear():
+    """The evaluator's list caches are rebuilt when a sampled user's list is edited in place (same
+    dict object, same length), and clear_caches() drops them."""
+    from factors_of_serendipity_recommendation_amd import evaluator
+    rng = np.random.default_rng(12)
+    n_items = 400
+
+    class DS:
+        def __init__(self):
+            self.testDict = {u: sorted(rng.choice(n_items, 4, replace=False).tolist()) for u in range(20)}
+            self._pos = {u: sorted(rng.choice(n_items, 5, replace=False).tolist()) for u in self.testDict}
+
+        def getUserPosItems(self, users):
+            return [self._pos[u] for u in users]
+
+    dev = torch.device("cpu")
+    ds = DS()
+    a = evaluator._TestLists.get(ds, n_items, dev)
+    assert evaluator._TestLists.get(ds, n_items, dev) is a
+    ds.testDict[3][-1] = n_items - 1 if ds.testDict[3][-1] != n_items - 1 else 0  # in place, same length
+    b = evaluator._TestLists.get(ds, n_items, dev)
+    assert b is not a
+    ds._pos[5].append(n_items - 2)  # the positives behind the mask change
+    c = evaluator._TestLists.get(ds, n_items, dev)
+    assert c is not b and evaluator._TestLists.get(ds, n_items, dev) is c
+    evaluator.clear_caches()
+    assert evaluator._TestLists.get(ds, n_items, dev) is not c
+
+    train = {u: sorted(rng.choice(500, 6, replace=False).tolist()) for u in range(40)}
+    test = {u: sorted(rng.choice(500, 3, replace=False).tolist()) for u in range(40)}
+    users = list(range(40))
+    x = evaluator._BatchLists.get(users, train, test, 0, dev)
+    train[0][0] = 499 if train[0][0] != 499 else 498
+    y = evaluator._BatchLists.get(users, train, test, 0, dev)
+    assert y is not x and evaluator._BatchLists.get(users, train, test, 0, dev) is y
+    evaluator.clear_caches()
+    assert evaluator._BatchLists.get(users, train, test, 0, dev) is not y

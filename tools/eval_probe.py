@@ -18,6 +18,7 @@ from factors_of_serendipity_recommendation_amd import _lib, ops  # noqa: E402
 if "--lib" in sys.argv:
     _lib.LIB_PATH = os.path.abspath(sys.argv[sys.argv.index("--lib") + 1])
     _lib._lib = None
+    _lib.ALLOW_MISSING = True
 ONLY = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
 DTYPES = (torch.float32,) if "--f32" in sys.argv else (torch.float32, torch.bfloat16)
 

@@ -1,9 +1,11 @@
 """Multi-GPU readiness on ONE GPU: the per-rank work of the C4 propagation at world = 8 (or --world),
-timed rank by rank with the real kernels, plus the per-layer collective volumes of
-distributed.ShardedPropagation.  Prints one JSON document with a predicted per-layer and per-step
-time at two assumed RCCL rates (one xGMI link, and the sum of the 7 links at an assumed efficiency).
+timed rank by rank with the real kernels and the real schedule of distributed.ShardedPropagation
+(push in n_chunks launches, pull, the rank-order slab sums, the item epilogue, K layers with the
+STACK mean in the last pull), with the collectives stubbed out.  Prints one JSON document: the
+per-rank phase times, the single-GPU step on the same graph, the collective volumes per layer, and
+a predicted step time and speedup at two assumed RCCL rates.
 
-  python tools/shard_probe.py [--world 8] [--ranks 0,7] [--dtype bf16] [--reps 3]
+  python tools/shard_probe.py [--world 8] [--ranks 0,7] [--dtype f32] [--reps 3] [--chunks 4]
 """
 import argparse
 import json
@@ -12,19 +14,31 @@ import sys
 import time
 
 import torch
+import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import factors_of_serendipity_recommendation_amd as lgx  # noqa: E402
-from factors_of_serendipity_recommendation_amd import _lib, ops  # noqa: E402
-from factors_of_serendipity_recommendation_amd.distributed import make_shard  # noqa: E402
-from factors_of_serendipity_recommendation_amd.synth import CONFIGS, synth_graph  # noqa: E402
+from factors_of_serendipity_recommendation_amd import ops  # noqa: E402
+from factors_of_serendipity_recommendation_amd.distributed import (ShardedPropagation,  # noqa: E402
+                                                                    make_shard_from_edges)
+from factors_of_serendipity_recommendation_amd.synth import CONFIGS, synth_edges, synth_graph  # noqa: E402
 
 LINK_GBS = 153.0       # one xGMI link per direction (task brief: 7 links x ~153 GB/s per GPU)
 LINKS = 7
 
 
-def timed(fn, reps):
+class _NoComm(ShardedPropagation):
+    """The product schedule with the exchanges and all-gathers left out (kernels only)."""
+
+    def _exchange(self, c0, m):
+        return None
+
+    def _all_gather(self, table):
+        return None
+
+
+def timed_steps(fn, reps):
     fn()
     torch.cuda.synchronize()
     best = float("inf")
@@ -42,74 +56,81 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--ranks", default="0,7")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--dtype", default="f32", choices=["bf16", "f32"])
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--chunks", type=int, default=4)
     ap.add_argument("--link-efficiency", type=float, default=0.6)
+    ap.add_argument("--no-one-gpu", action="store_true")
     args = ap.parse_args()
     cfg = CONFIGS["synth10m"]
     U, I, d, K, w = cfg.n_users, cfg.n_items, cfg.d, cfg.K, args.world
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     s = 2 if dt == torch.bfloat16 else 4
-    t0 = time.time()
-    A = synth_graph(cfg, seed=2020, device="cuda")
-    print(f"graph nnz={A.nnz} in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
-    # the single-GPU layer for reference (same graph, same kernels)
+    # a one-process gloo group: ShardedPropagation asks the backend; no collective is issued
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29611")
+    dist.init_process_group("gloo", rank=0, world_size=1)
     E0 = lgx.fill_normal((U + I, d), 0.1, 2020, dtype=dt)
-    Y = torch.empty_like(E0)
-    acc = torch.zeros((U + I, d), dtype=torch.float32, device="cuda")
-    out = torch.empty((U + I, d), dtype=torch.float32, device="cuda")
-    one_gpu = timed(lambda: ops.propagate_layer(A, E0, _lib.LGX_LAYER_MID, Y=Y, E0=E0, acc=acc, out=out,
-                                                n_mean=float(K + 1)), args.reps)
-    del Y, acc, out
-    torch.cuda.empty_cache()
+    one_gpu = None
+    if not args.no_one_gpu:
+        t0 = time.time()
+        A = synth_graph(cfg, seed=2020, device="cuda")
+        print(f"graph nnz={A.nnz} in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+        out = torch.empty((U + I, d), dtype=torch.float32, device="cuda")
+        one_gpu = timed_steps(lambda: ops.propagate(A, E0, K, out=out), args.reps)
+        print(f"one GPU step {one_gpu:.2f} ms", file=sys.stderr, flush=True)
+        del A, out
+        torch.cuda.empty_cache()
+    u, i = synth_edges(cfg, seed=2020, device="cuda")
     ranks = []
     for r in (int(x) for x in args.ranks.split(",")):
         t0 = time.time()
-        sh = make_shard(A, U, I, r, w)
+        sh = make_shard_from_edges(u, i, U, I, r, w)
         build = time.time() - t0
-        nu, mi = sh.n_u_local, sh.mi
-        Xu = lgx.fill_normal((nu, d), 0.1, 7 + r, dtype=dt)
-        Xi = lgx.fill_normal((w * mi, d), 0.1, 11, dtype=dt)
-        P = torch.empty((w * mi, d), dtype=torch.float32, device="cuda")
-        Yu = torch.empty((nu, d), dtype=dt, device="cuda")
-        acc_u = torch.zeros((nu, d), dtype=torch.float32, device="cuda")
-        out_u = torch.empty((nu, d), dtype=torch.float32, device="cuda")
-        yi = torch.randn((mi, d), dtype=torch.float32, device="cuda")
-        Yi = torch.empty((mi, d), dtype=dt, device="cuda")
-        acc_i = torch.zeros((mi, d), dtype=torch.float32, device="cuda")
-        out_i = torch.empty((mi, d), dtype=torch.float32, device="cuda")
-        E0i = Xi[:mi]
-        push = timed(lambda: ops.propagate_layer(sh.A_push, Xu, _lib.LGX_LAYER_PARTIAL, out=P), args.reps)
-        pull = timed(lambda: ops.propagate_layer(sh.A_pull, Xi, _lib.LGX_LAYER_MID, Y=Yu, E0=Xu, acc=acc_u,
-                                                 out=out_u, n_mean=float(K + 1)), args.reps)
-        epi = timed(lambda: ops.layer_epilogue(yi, _lib.LGX_LAYER_MID, Y=Yi, E0=E0i, acc=acc_i, out=out_i,
-                                               n_mean=float(K + 1)), args.reps)
-        rs_bytes = (w - 1) / w * (w * mi) * d * 4      # reduce-scatter of the fp32 push partials
-        ag_bytes = (w - 1) / w * (w * mi) * d * s      # all-gather of the item block of the layer
-        ranks.append({"rank": r, "users": nu, "pull_nnz": sh.A_pull.nnz, "push_nnz": sh.A_push.nnz,
-                      "shard_build_s": round(build, 2), "push_ms": push, "pull_ms": pull, "item_epilogue_ms": epi,
-                      "reduce_scatter_bytes": int(rs_bytes), "all_gather_bytes": int(ag_bytes)})
-        print(json.dumps(ranks[-1]), file=sys.stderr, flush=True)
-        del sh, Xu, Xi, P, Yu, acc_u, out_u, yi, Yi, acc_i, out_i
+        prop = _NoComm(sh, E0[:U], E0[U:], K, force_collectives=True, n_chunks=args.chunks)
+        step_ms = timed_steps(prop.step, args.reps)
+        prop.record_phases = True
+        for _ in range(args.reps):
+            prop.step()
+        ph = prop.phase_summary()
+        mi = sh.mi
+        a2a_bytes = (w - 1) / w * (w * mi) * d * 4       # fp32 push partials out (and in) per layer
+        ag_bytes = (w - 1) * mi * d * s                  # item blocks received per layer
+        rec = {"rank": r, "users": sh.n_u_local, "pull_nnz": sh.A_pull.nnz, "push_nnz": sh.A_push.nnz,
+               "push_chunks": len(prop.push_chunks), "shard_build_s": round(build, 2), "step_ms": step_ms,
+               "phases_ms_per_step": {k: v for k, v in ph.items() if k in ("push", "pull", "reduce", "epilogue")},
+               "all_to_all_bytes_per_layer": int(a2a_bytes), "all_gather_bytes_per_layer": int(ag_bytes)}
+        ranks.append(rec)
+        print(json.dumps(rec), file=sys.stderr, flush=True)
+        del sh, prop
         torch.cuda.empty_cache()
-    worst = max(ranks, key=lambda x: x["push_ms"] + x["pull_ms"] + x["item_epilogue_ms"])
-    compute = worst["push_ms"] + worst["pull_ms"] + worst["item_epilogue_ms"]
+    worst = max(ranks, key=lambda x: x["step_ms"])
+    ph = worst["phases_ms_per_step"]
+    push_l, pull_l = ph["push"] / K, ph["pull"] / K
+    nch = worst["push_chunks"]
     pred = {}
-    for name, gbs in (("one_link", LINK_GBS), (f"{LINKS}_links_x{args.link_efficiency}", LINKS * LINK_GBS * args.link_efficiency)):
-        rs = worst["reduce_scatter_bytes"] / gbs / 1e6
-        ag = worst["all_gather_bytes"] / gbs / 1e6
-        # schedule (distributed.py): RS(k) hides under pull(k), AG(k) under push(k+1); exposed = the excess
-        exposed = max(0.0, rs - worst["pull_ms"]) + max(0.0, ag - worst["push_ms"])
-        layer = compute + exposed
-        step = K * compute + max(0.0, rs - worst["pull_ms"]) * K + max(0.0, ag - worst["push_ms"]) * (K - 1)
-        pred[name] = {"rccl_GBs_assumed": gbs, "reduce_scatter_ms": rs, "all_gather_ms": ag,
-                      "exposed_comm_ms_per_layer": exposed, "layer_ms": layer, "step_ms": step,
-                      "speedup_vs_1gpu": (K * one_gpu) / step}
-    print(json.dumps({"workload": f"synth10m {args.dtype} K={K} d={d}, world={w}", "one_gpu_layer_ms": one_gpu,
-                      "ranks": ranks, "critical_rank": worst["rank"], "compute_ms_per_layer": compute,
+    for name, per_peer_gbs in (("one_link_total", LINK_GBS / (w - 1)),
+                               (f"{LINKS}_links_x{args.link_efficiency}", LINK_GBS * args.link_efficiency)):
+        # all-to-all: each peer pair has its own link, carrying 1/(w-1) of the out bytes; all-gather:
+        # one block from each peer.  "one_link_total" = the whole volume through one link's rate.
+        a2a = worst["all_to_all_bytes_per_layer"] / (w - 1) / per_peer_gbs / 1e6
+        ag = worst["all_gather_bytes_per_layer"] / (w - 1) / per_peer_gbs / 1e6
+        # schedule: chunk c's exchange starts after its push launch and must end before the
+        # reduce; it runs under the later chunks' pushes and the pull.  The all-gather of layer k
+        # runs under the push of layer k+1 (K-1 of them per step).
+        window_a2a = push_l * (nch - 1) / nch + pull_l
+        exposed = K * max(0.0, a2a - window_a2a) + (K - 1) * max(0.0, ag - push_l)
+        step = worst["step_ms"] + exposed
+        pred[name] = {"per_peer_GBs_assumed": per_peer_gbs, "all_to_all_ms_per_layer": a2a,
+                      "all_gather_ms_per_layer": ag, "exposed_comm_ms_per_step": exposed, "step_ms": step,
+                      "speedup_vs_1gpu": (one_gpu / step) if one_gpu else None}
+    print(json.dumps({"workload": f"synth10m {args.dtype} K={K} d={d}, world={w}", "one_gpu_step_ms": one_gpu,
+                      "ranks": ranks, "critical_rank": worst["rank"], "kernel_ms_per_step": worst["step_ms"],
                       "prediction": pred,
-                      "note": "per-rank kernels timed on one MI355X (HIP events, best of reps); collective "
-                              "times are volumes / assumed RCCL rates, not measurements"}, indent=1), flush=True)
+                      "note": "per-rank kernels of ShardedPropagation.step (collectives stubbed out) timed on one "
+                              "MI355X with HIP events, best of reps; collective times are volumes / assumed "
+                              "RCCL rates, not measurements"}, indent=1), flush=True)
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":
