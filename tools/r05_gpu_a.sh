@@ -8,8 +8,26 @@ OUT=gpurun_out/r05a
 mkdir -p $OUT
 NEW=factors_of_serendipity_recommendation_amd/liblgx.so
 OLD=tools/_ab/liblgx_r04.so
+# bf16 C5 scoring: L2-miss bytes (FETCH_SIZE, its own pass per build) and time of the round-3 final,
+# round-4 final, this build without the round-4 refill placement, and this build
+export TMPDIR=/tmp
+for lib in tools/_ab/liblgx_r03.so $OLD tools/_ab/liblgx_norefill.so $NEW; do
+  n=$(basename $lib .so)
+  timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "score_topk" --output-format csv \
+      -d $OUT/fetch_$n -o run -- python3 tools/score_traffic.py --lib $lib --calls 1 > $OUT/fetch_$n.json 2> $OUT/fetch_$n.log \
+      || { tail -20 $OUT/fetch_$n.log; exit 1; }
+  python3 tools/fetch_sum.py $OUT/fetch_$n 2 >> $OUT/fetch_summary.jsonl
+  rm -rf $OUT/fetch_$n
+done
+for rep in 1 2; do
+  for lib in tools/_ab/liblgx_r03.so $OLD tools/_ab/liblgx_norefill.so $NEW; do
+    timeout -k 10 180 python3 tools/score_traffic.py --lib $lib --calls 3 >> $OUT/score_ab.jsonl 2>> $OUT/score_ab.log \
+        || { tail -20 $OUT/score_ab.log; exit 1; }
+  done
+done
+cat $OUT/fetch_summary.jsonl $OUT/score_ab.jsonl
 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
-    tests/test_gpu_score_f32.py tests/test_gpu_topk_eval.py tests/test_gpu_stratify.py \
+    tests/test_gpu_score_f32.py tests/test_gpu_topk_eval.py tests/test_gpu_stratify.py tests/test_gpu_sigmoid.py \
     "tests/test_gpu_parity.py::test_batch_test_both_flags_vs_oracle" \
     "tests/test_gpu_parity.py::test_column_mean_is_numpy_mean_bit_for_bit" \
     tests/test_gpu_pinned.py -k "not full_size and not c3_amazon and not c1_gowalla" \
