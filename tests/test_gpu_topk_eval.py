@@ -165,4 +165,4 @@ def test_procedure_test_matches_oracle_restatement(mlls, tmp_path, topks, d):
     for key in ("recall", "precision"):
         assert np.allclose(got[key], ref[key] / len(users), rtol=0, atol=1e-12), (key, got[key], ref[key])
     assert np.allclose(got["ndcg"], ref["ndcg"] / len(users), rtol=1e-6, atol=0), (got["ndcg"], ref["ndcg"])
-    assert got["recall"][1] > got["recall"][0] > 0
+    assert got["recall"][-1] >= got["recall"][0] > 0
