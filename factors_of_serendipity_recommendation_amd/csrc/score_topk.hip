@@ -95,7 +95,7 @@ struct ScoreArgs {
     float* part_score;    // [B, n_splits, k]
     int32_t* part_idx;    // [B, n_splits, k]
     uint32_t* minmax;     // ordered {min, max} or nullptr
-    uint64_t* susp;       // [B, 2, kSuspSlots] parked keys (LDS kernel, full sweep), or nullptr
+    uint64_t* susp;       // [B, n_splits, 2, kSuspSlots] parked keys (LDS kernel), or nullptr
     // seeded sweep (LDS kernel, full sweep): each user's exact top-k over items [0, seed_items),
     // [B, k] (index -1 = empty); the sweep then covers [seed_items, n_items) only
     const float* seed_score;
@@ -112,7 +112,7 @@ struct ScoreArgs {
 // sweep is a chain of dependent global loads that also waits for the in-flight tile DMA (vmcnt
 // completes in order), and the per-tile barrier makes every wave of the workgroup wait for it.  A
 // lane with all its slots taken searches at once, as before.
-constexpr int kSuspSlots = 24;
+constexpr int kSuspSlots = 32;  // per (user, split, lane half); resolve_suspects' keep mask is 32 bits
 constexpr int kBloomWords = 8;  // 256-bit filter: 8 VGPRs
 constexpr int kBloomShift = 32 - 5 - 3;
 
@@ -185,7 +185,8 @@ struct WaveTopKT {
     float tau;       // filter threshold: -inf until the list is full, +inf for padding users
     int32_t tau_i;
     float mn, mx;
-    bool park;       // parked keys enabled (full-sweep LDS kernel with a mask); count in LDS (scnt())
+    bool park;       // parked keys enabled (LDS kernel with a mask); count in LDS (scnt())
+    int sp;          // catalog split of this workgroup (its parked keys' region)
     // 256-bit Bloom filter of the user's masked items (2 hashes; false-positive rate ~10% at 50
     // masked items), as 16 scalars so that the word select stays in registers
     uint32_t bl[kBloomWords];
@@ -269,9 +270,13 @@ struct WaveTopKT {
         if (len == k) rescan();
         refresh_tau();
     }
-    // full-sweep launches only (one workgroup per user); split lists test at once
-    __device__ __forceinline__ void enable_suspects(const ScoreArgs& a) {
-        park = a.susp && a.mask_indptr && a.n_splits == 1;  // wave-uniform
+    // every LDS launch with a mask: each (user, split) has its own region, so the splits of a
+    // split launch park too.  With propagated LightGCN tables a user's masked (train) items are
+    // among its best scores, so each of them reaches the filter once per sweep: searched at once in
+    // the sweep that is a chain of dependent global loads per masked item (Procedure.Test's shapes)
+    __device__ __forceinline__ void enable_suspects(const ScoreArgs& a, int split) {
+        park = a.susp && a.mask_indptr;  // wave-uniform
+        sp = split;
         if (park) *scnt() = 0;
     }
     // this lane's parked-key count: the int after the wave's pending slots (list_bytes_per_wave)
@@ -281,7 +286,7 @@ struct WaveTopKT {
     }
     // recomputed on use (rare) instead of held in registers
     __device__ __forceinline__ uint64_t* susp_slots(const ScoreArgs& a) const {
-        return a.susp + ((size_t)b * 2 + h) * kSuspSlots;
+        return a.susp + (((size_t)b * a.n_splits + sp) * 2 + h) * kSuspSlots;
     }
 
     // new worst entry: 8 keys (four 16-byte reads issued together) per LDS round trip
@@ -831,7 +836,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     }
     TopK st;
     st.init(lk, lk + list_keys_per_wave(k), k, lane, b, user_ok);
-    st.enable_suspects(a);
+    st.enable_suspects(a, split);
     st.build_bloom(a);
     if (a.seed_score) st.seed(a);
     else if (MODE != kFloorOnly && a.floor && user_ok) st.tau = a.floor[b * a.n_splits + split];
@@ -1855,7 +1860,7 @@ struct UserRange {
 // workspace of one range: the split lists (scores, then indices), then the LDS kernel's parked keys
 size_t range_list_bytes(const UserRange& r, int k) { return align_up((size_t)(r.u1 - r.u0) * r.p.n_splits * k * 4); }
 size_t range_susp_bytes(const UserRange& r) {
-    return r.p.lds && r.p.n_splits == 1 ? align_up((size_t)(r.u1 - r.u0) * 2 * kSuspSlots * 8) : 0;
+    return r.p.lds ? align_up((size_t)(r.u1 - r.u0) * r.p.n_splits * 2 * kSuspSlots * 8) : 0;
 }
 // the LDS kernel's score floors [users, n_splits]
 size_t range_floor_bytes(const UserRange& r) { return r.p.lds ? align_up((size_t)(r.u1 - r.u0) * r.p.n_splits * 4) : 0; }

@@ -231,24 +231,51 @@ __global__ __launch_bounds__(kFoldUsers) void foldout_staged_kernel(const int32_
 
 // np.mean(a, axis=0) of a C-contiguous float32 [rows, cols] array, as numpy computes it: per column a
 // float32 sum over the rows in row order (numpy's axis-0 add.reduce adds whole rows, no pairwise
-// blocking), then one float32 division by the row count.  One lane per column, so a row step is one
-// coalesced read per wave; the loads run ahead of the dependent adds.
-__global__ __launch_bounds__(64) void column_mean_kernel(const float* __restrict__ src, int64_t rows, int64_t cols,
-                                                        float* __restrict__ out) {
-    const int64_t j = blockIdx.x * (int64_t)64 + threadIdx.x;
-    if (j >= cols) return;
-    const float* p = src + j;
-    float acc = 0.0f;
-    int64_t i = 0;
-    for (; i + 8 <= rows; i += 8) {
-        float v[8];
+// blocking), then one float32 division by the row count.  The order makes each column one chain of
+// dependent adds; what must not sit on that chain is the load latency.  A workgroup owns 64 columns:
+// its 256 threads stage blocks of kMeanRows rows into LDS (coalesced 256-B row pieces, the next block
+// in flight while the current one is summed) and wave 0 adds them lane = column, row by row.
+constexpr int kMeanRows = 128;
+__global__ __launch_bounds__(256) void column_mean_kernel(const float* __restrict__ src, int64_t rows, int64_t cols,
+                                                         float* __restrict__ out) {
+    __shared__ float blk[2][kMeanRows][64];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int64_t c0 = (int64_t)blockIdx.x * 64;
+    const int64_t col = c0 + lane;
+    float nx[kMeanRows / 4];
+    auto load = [&](int64_t r0) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = p[(i + q) * cols];
+        for (int j = 0; j < kMeanRows / 4; ++j) {
+            const int64_t r = r0 + 4 * j + w;
+            nx[j] = (r < rows && col < cols) ? src[r * cols + col] : 0.0f;
+        }
+    };
+    auto store = [&](int b) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) acc = acc + v[q];
+        for (int j = 0; j < kMeanRows / 4; ++j) blk[b][4 * j + w][lane] = nx[j];
+    };
+    float acc = -0.0f;  // -0 + x == x for every x: the same sums as numpy's, which starts from row 0
+    load(0);
+    store(0);
+    __syncthreads();
+    int b = 0;
+    for (int64_t r0 = 0; r0 < rows; r0 += kMeanRows) {
+        const bool more = r0 + kMeanRows < rows;
+        if (more) load(r0 + kMeanRows);
+        if (w == 0) {
+            const int n = (int)min((int64_t)kMeanRows, rows - r0);
+            if (n == kMeanRows) {
+#pragma unroll 16
+                for (int r = 0; r < kMeanRows; ++r) acc = acc + blk[b][r][lane];
+            } else {
+                for (int r = 0; r < n; ++r) acc = acc + blk[b][r][lane];
+            }
+        }
+        if (more) store(b ^ 1);
+        __syncthreads();
+        b ^= 1;
     }
-    for (; i < rows; ++i) acc = acc + p[i * cols];
-    out[j] = rows > 0 ? acc / (float)rows : NAN;
+    if (w == 0 && col < cols) out[col] = rows > 0 ? acc / (float)rows : NAN;
 }
 
 template <int R>
@@ -309,7 +336,7 @@ extern "C" int lgx_column_mean_f32(const float* src, int64_t rows, int64_t cols,
     LGX_REQUIRE(rows < (1LL << 24), LGX_ERR_UNSUPPORTED,
                 "lgx_column_mean_f32: %lld rows (the float32 row count is exact below 2^24)", (long long)rows);
     if (cols == 0) return LGX_OK;
-    column_mean_kernel<<<(unsigned)ceil_div(cols, (int64_t)64), 64, 0, as_hip(stream)>>>(src, rows, cols, out);
+    column_mean_kernel<<<(unsigned)ceil_div(cols, (int64_t)64), 256, 0, as_hip(stream)>>>(src, rows, cols, out);
     LGX_LAUNCH_CHECK();
     return LGX_OK;
 }
