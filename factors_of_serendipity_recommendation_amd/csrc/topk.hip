@@ -155,6 +155,24 @@ struct TruthRegs {
     }
 };
 
+// a long truth list (more than kTruthRegs items) against up to 32 ranks: the list is streamed once
+// (independent loads) and each item compared with the ranks held in registers, instead of a scan of
+// the list per rank.  A power-law user with 1000 test items made that scan 20 000 loads in one lane,
+// and its wave the kernel's tail (batch_test at the Gowalla shape: 2.5 ms for 27 522 users).
+constexpr int kStreamRanks = 32;
+__device__ __forceinline__ uint32_t hit_bits_streamed(const int32_t* rank, int k, const int32_t* truth, int64_t tl) {
+    int32_t rr[kStreamRanks];
+#pragma unroll
+    for (int i = 0; i < kStreamRanks; ++i) rr[i] = i < k ? rank[i] : -2;  // bits past k are cleared below
+    uint32_t bits = 0;
+    for (int64_t j = 0; j < tl; ++j) {
+        const int32_t x = truth[j];
+#pragma unroll
+        for (int i = 0; i < kStreamRanks; ++i) bits |= rr[i] == x ? (1u << i) : 0u;
+    }
+    return bits & (k >= 32 ? ~0u : ((1u << k) - 1u));
+}
+
 // evaluate_foldout.h:16-112 per user; float accumulators with double increments as in the C++.
 // out[c * ostride + i] for curve c (precision, recall, map, ndcg, mrr) at rank i.
 __device__ __forceinline__ void foldout_user(const int32_t* rank, const int32_t* truth, int64_t tl, int k,
@@ -163,9 +181,12 @@ __device__ __forceinline__ void foldout_user(const int32_t* rank, const int32_t*
     float sum_pre = 0.0f, dcg = 0.0f, idcg = 0.0f;
     bool found = false;
     TruthRegs tr;
-    tr.load(truth, tl);
+    const bool streamed = tl > kTruthRegs && k <= kStreamRanks;
+    uint32_t hb = 0;
+    if (streamed) hb = hit_bits_streamed(rank, k, truth, tl);
+    else tr.load(truth, tl);
     for (int i = 0; i < k; ++i) {
-        const bool hit = tr.has(rank[i]);
+        const bool hit = streamed ? ((hb >> i) & 1u) != 0u : tr.has(rank[i]);
         if (hit) {
             hits += 1;
             const float pre = (float)(1.0 * hits / (i + 1));

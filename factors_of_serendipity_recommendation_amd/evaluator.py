@@ -212,9 +212,12 @@ class _BatchLists:
 
     _cache: Dict[tuple, "_BatchLists"] = {}
 
-    def __init__(self, users: np.ndarray, train_items, test_set, flag: int, dev):
+    def __init__(self, users_to_test, users: np.ndarray, train_items, test_set, flag: int, dev):
         self.train_items, self.test_set, self.users = train_items, test_set, users  # held (ids stay valid)
+        self.users_obj = users_to_test  # the caller's sequence: the same object skips the O(n) compare
         ul = users.tolist()
+        self.user_probe = _sample_keys(list(range(len(ul))))
+        self.user_stamp = tuple(ul[i] for i in self.user_probe)
         self.probe = _sample_keys(ul)
         self.stamp = self.fingerprint()
         self.rows = torch.as_tensor(users, dtype=torch.int64, device=dev)
@@ -235,13 +238,20 @@ class _BatchLists:
 
     @classmethod
     def get(cls, users_to_test, train_items, test_set, flag: int, dev) -> "_BatchLists":
-        users = np.fromiter((int(u) for u in users_to_test), dtype=np.int64)
-        key = (id(train_items), id(test_set), len(users), flag, str(dev))
+        key = (id(train_items), id(test_set), len(users_to_test), flag, str(dev))
         hit = cls._cache.get(key)
-        if (hit is None or hit.train_items is not train_items or hit.test_set is not test_set
-                or not np.array_equal(hit.users, users) or hit.fingerprint() != hit.stamp):
-            cls._cache.clear()
-            hit = cls._cache[key] = cls(users, train_items, test_set, flag, dev)
+        if hit is not None and hit.train_items is train_items and hit.test_set is test_set:
+            # the same users: the same sequence object with its sampled entries unchanged (the
+            # reference passes data_generator's list every time), or equal contents
+            if hit.users_obj is users_to_test and len(users_to_test) == len(hit.users):
+                same = all(int(users_to_test[i]) == v for i, v in zip(hit.user_probe, hit.user_stamp))
+            else:
+                same = np.array_equal(hit.users, np.fromiter((int(u) for u in users_to_test), dtype=np.int64))
+            if same and hit.fingerprint() == hit.stamp:
+                return hit
+        users = np.fromiter((int(u) for u in users_to_test), dtype=np.int64)
+        cls._cache.clear()
+        hit = cls._cache[key] = cls(users_to_test, users, train_items, test_set, flag, dev)
         return hit
 
 
