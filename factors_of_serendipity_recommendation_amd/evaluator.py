@@ -127,6 +127,50 @@ def clear_caches() -> None:
     _BatchLists._cache.clear()
 
 
+# Users whose mask holds more than this many items are ranked by the dense route
+# (ops.score_topk_dense_masked) when the catalog is small enough for dense rows (the evaluation
+# shapes): their 256-bit Bloom filter is saturated, so in the fused walk every one of their masked
+# items that reaches the running threshold takes an exact search.  On propagated LightGCN tables a
+# user's train items are among its best scores, and power-law users mask thousands of them
+# (tools/mask_probe.py, profiles/r05_mask_probe.txt: the ~5 % of Gowalla-shape users above 64 masked
+# items cost 1.6 ms of the 5.1 ms fused launch).
+DENSE_MASK_MIN = 64
+DENSE_MAX_ITEMS = 1 << 18
+
+
+class _Route:
+    """The split of an evaluation set between the fused launch and the dense route."""
+
+    def __init__(self, rows: torch.Tensor, mask, n_items: int, k_max: int):
+        self.rows, self.mask = rows, mask
+        n = rows.numel()
+        lens = (mask[0][1:] - mask[0][:-1]) if mask is not None else None
+        heavy = torch.zeros(n, dtype=torch.bool, device=rows.device)
+        if lens is not None and n_items <= DENSE_MAX_ITEMS:
+            heavy = (lens > DENSE_MASK_MIN) & (lens <= n_items - k_max)
+        self.n_heavy = int(heavy.sum())
+        if self.n_heavy == 0:
+            self.light_pos = None
+            return
+        self.light_pos = torch.nonzero(~heavy).flatten()
+        self.heavy_pos = torch.nonzero(heavy).flatten()
+        self.light_rows, self.heavy_rows = rows[self.light_pos].contiguous(), rows[self.heavy_pos].contiguous()
+        self.light_mask = ops.csr_rows(mask, self.light_pos)
+        self.heavy_mask = ops.csr_rows(mask, self.heavy_pos)
+
+    def topk(self, users: torch.Tensor, items: torch.Tensor, k: int, mask_value: float, apply_sigmoid: bool):
+        """idx int32 [n, k] for every user of the set, in set order."""
+        if self.light_pos is None:
+            return ops.score_topk(users, items, k, user_rows=self.rows, mask=self.mask, mask_value=mask_value,
+                                  apply_sigmoid=apply_sigmoid)[0]
+        idx = torch.empty((self.rows.numel(), k), dtype=torch.int32, device=users.device)
+        if self.light_pos.numel():
+            idx[self.light_pos] = ops.score_topk(users, items, k, user_rows=self.light_rows, mask=self.light_mask,
+                                                 mask_value=mask_value, apply_sigmoid=apply_sigmoid)[0]
+        idx[self.heavy_pos] = ops.score_topk_dense_masked(users, items, k, self.heavy_rows, self.heavy_mask)
+        return idx
+
+
 class _TestLists:
     """The static lists of one evaluation set on the device: the test users (row ids), their train
     positives (the mask CSR) and their test items as sorted (row * M + item) keys.  Procedure.Test
@@ -146,6 +190,7 @@ class _TestLists:
         self.mask = ops.lists_to_device_csr(dataset.getUserPosItems(self.users), dev, sort=True)
         self.probe = _sample_keys(self.users)
         self.stamp = self.fingerprint(dataset)
+        self.routes: Dict[tuple, _Route] = {}
         truths = [testDict[u] for u in self.users]
         self.recall_n = np.fromiter(map(len, truths), dtype=np.int64, count=n)
         self.recall_n_dev = torch.from_numpy(self.recall_n).to(dev)
@@ -153,6 +198,12 @@ class _TestLists:
         self.M = int(max(n_items, int(flat.max()) + 1 if flat.size else 0, 1))
         keys = np.repeat(np.arange(n, dtype=np.int64), self.recall_n) * self.M + flat
         self.keys = torch.unique(torch.from_numpy(keys).to(dev))  # sorted
+
+    def route(self, n_items: int, k: int) -> _Route:
+        key = (n_items, k)
+        if key not in self.routes:
+            self.routes[key] = _Route(self.rows, self.mask, n_items, k)
+        return self.routes[key]
 
     def fingerprint(self, dataset) -> tuple:
         try:
@@ -194,8 +245,7 @@ def Test(dataset, Recmodel, epoch=0, w=None, multicore=0, topks: Sequence[int] =
     with torch.no_grad():
         all_users, all_items = Recmodel.computer()
         tl = _TestLists.get(dataset, all_items.shape[0], all_users.device)
-        idx, _ = ops.score_topk(all_users, all_items, max_K, user_rows=tl.rows, mask=tl.mask,
-                                mask_value=-float(1 << 10), apply_sigmoid=True)
+        idx = tl.route(all_items.shape[0], max_K).topk(all_users, all_items, max_K, -float(1 << 10), True)
         res = _metrics_dev(tl.hit_mask(idx), tl.recall_n_dev, topks)
         for key in results:
             results[key] = res[key] / float(len(tl.users))
@@ -228,6 +278,13 @@ class _BatchLists:
             truths = [train_items[u] for u in ul]
             self.mask = None
         self.truth = ops.lists_to_device_csr(truths, dev, sort=False)
+        self.routes: Dict[tuple, _Route] = {}
+
+    def route(self, n_items: int, k: int) -> _Route:
+        key = (n_items, k)
+        if key not in self.routes:
+            self.routes[key] = _Route(self.rows, self.mask, n_items, k)
+        return self.routes[key]
 
     def fingerprint(self) -> tuple:
         try:
@@ -266,7 +323,7 @@ def batch_test(user_emb: torch.Tensor, item_emb: torch.Tensor, users_to_test: Se
     top_show = np.sort(np.asarray(Ks))
     max_top = int(max(top_show))
     bl = _BatchLists.get(users_to_test, train_items, test_set, train_set_flag, user_emb.device)
-    idx, _ = ops.score_topk(user_emb, item_emb, max_top, user_rows=bl.rows, mask=bl.mask, mask_value=float("-inf"))
+    idx = bl.route(item_emb.shape[0], max_top).topk(user_emb, item_emb, max_top, float("-inf"), False)
     curves = ops.foldout_metrics(idx, bl.truth)
     # the users' mean on the device: only 5 x max_top values cross to the host
     mean = ops.column_mean(curves).cpu().numpy()

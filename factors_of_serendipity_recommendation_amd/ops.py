@@ -257,6 +257,42 @@ def score_topk(Q: torch.Tensor, items: torch.Tensor, k: int, user_rows: Optional
     return (idx, val, mm) if want_minmax else (idx, val)
 
 
+def csr_rows(csr: Tuple[torch.Tensor, torch.Tensor], sel: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Rows `sel` (int64, device) of a device CSR (indptr int64, indices), in that order."""
+    ip, ix = csr
+    lens = (ip[1:] - ip[:-1])[sel]
+    nip = torch.zeros(sel.numel() + 1, dtype=torch.int64, device=ip.device)
+    torch.cumsum(lens, 0, out=nip[1:])
+    rid = torch.repeat_interleave(torch.arange(sel.numel(), device=ip.device), lens)
+    pos = ip[sel][rid] + torch.arange(rid.numel(), device=ip.device) - nip[rid]
+    return nip, ix[pos].contiguous()
+
+
+def score_topk_dense_masked(Q: torch.Tensor, items: torch.Tensor, k: int, user_rows: torch.Tensor,
+                            mask: Tuple[torch.Tensor, torch.Tensor], chunk_bytes: int = 256 << 20) -> torch.Tensor:
+    """The ranking score_topk returns (idx int32 [B, k]; raw scores ranked, ties to the lower item id)
+    by another route, for users whose mask is long: their dense raw score rows (lgx_score_dense), the
+    masked entries set to -inf, the row top-k (lgx_topk_rows).  In the fused walk every masked item
+    of such a user that reaches the running threshold needs an exact test (its 256-bit Bloom filter is
+    saturated); here a mask costs one scattered store per item.  Every user must keep at least k
+    unmasked items (the fused path's masked tail is not reproduced).  Users go in chunks of at most
+    chunk_bytes of scores."""
+    require_gpu(Q, items, user_rows)
+    B, I = user_rows.numel(), items.shape[0]
+    idx = torch.empty((B, k), dtype=torch.int32, device=Q.device)
+    step = max(1, chunk_bytes // max(1, 4 * I))
+    for c0 in range(0, B, step):
+        c1 = min(B, c0 + step)
+        sel = torch.arange(c0, c1, device=Q.device)
+        S = score_dense(Q, items, user_rows=user_rows[c0:c1])
+        ip, ix = csr_rows(mask, sel)
+        rid = torch.repeat_interleave(torch.arange(c1 - c0, device=Q.device), ip[1:] - ip[:-1])
+        S.view(-1).index_fill_(0, rid * I + ix.to(torch.int64), float("-inf"))
+        idx[c0:c1] = topk_rows(S, k)[0]
+        del S
+    return idx
+
+
 def score_minmax(Q: torch.Tensor, items: torch.Tensor, user_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Global (min, max) of Q . items^T over every pair (``lgx_score_minmax``) -> f32 [2] on the
     device (recommend.py:163-164, :375-377)."""

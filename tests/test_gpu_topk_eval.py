@@ -166,3 +166,61 @@ def test_procedure_test_matches_oracle_restatement(mlls, tmp_path, topks, d):
         assert np.allclose(got[key], ref[key] / len(users), rtol=0, atol=1e-12), (key, got[key], ref[key])
     assert np.allclose(got["ndcg"], ref["ndcg"] / len(users), rtol=1e-6, atol=0), (got["ndcg"], ref["ndcg"])
     assert got["recall"][-1] >= got["recall"][0] > 0
+
+
+@pytest.mark.parametrize("d", [64, 128])
+def test_dense_masked_route_matches_float64(d):
+    """ops.score_topk_dense_masked (the evaluator's route for users with long masks: dense raw scores,
+    masked entries -inf, row top-k) returns k distinct unmasked items, each within 1e-5 of the exact
+    k-th best unmasked score, for masks of 65..3000 items; chunked over users."""
+    g = torch.Generator(device=DEV).manual_seed(d)
+    B, I, k = 300, 20_000, 20
+    Q = torch.randn(B + 50, d, device=DEV, generator=g) / 8
+    items = torch.randn(I, d, device=DEV, generator=g) / 8
+    rows = torch.randperm(B + 50, device=DEV, generator=g)[:B]
+    lens = torch.randint(65, 3000, (B,), generator=torch.Generator().manual_seed(d)).tolist()
+    # each user's best items masked first, so the mask hits the scores that matter
+    S = Q[rows].double() @ items.double().T
+    order = torch.argsort(S, dim=1, descending=True)
+    lists = [sorted(order[u, :lens[u]].tolist()) for u in range(B)]
+    mask = ops.lists_to_device_csr(lists, DEV)
+    idx = ops.score_topk_dense_masked(Q, items, k, rows, mask, chunk_bytes=64 * I * 4)
+    for u in range(B):
+        S[u, torch.tensor(lists[u], device=DEV)] = float("-inf")
+    kth = torch.topk(S, k, dim=1).values[:, -1:]
+    got = S.gather(1, idx.long())
+    assert torch.isfinite(got).all(), "a masked item was returned"
+    assert (got >= kth - 1e-5 * kth.abs().clamp(min=1.0)).all()
+    srt = idx.long().sort(1).values
+    assert (srt[:, 1:] != srt[:, :-1]).all()
+
+
+def test_evaluator_route_splits_long_masks():
+    """evaluator._Route: users with more than DENSE_MASK_MIN masked items (and at least k unmasked)
+    go to the dense route, the rest to the fused launch; both results land in set order and agree
+    with the fused launch over everyone as top-k sets."""
+    from factors_of_serendipity_recommendation_amd.evaluator import DENSE_MASK_MIN, _Route
+    g = torch.Generator(device=DEV).manual_seed(3)
+    B, I, d, k = 2000, 30_000, 64, 20
+    Q = torch.randn(B, d, device=DEV, generator=g) / 8
+    items = torch.randn(I, d, device=DEV, generator=g) / 8
+    rng = np.random.default_rng(3)
+    lens = np.where(rng.random(B) < 0.1, rng.integers(DENSE_MASK_MIN + 1, 5000, B), rng.integers(0, 40, B))
+    lens[7] = I - k + 1  # fewer than k unmasked items: stays on the fused path (its masked tail)
+    lists = [sorted(rng.choice(I, int(n), replace=False).tolist()) for n in lens]
+    mask = ops.lists_to_device_csr(lists, DEV)
+    rows = torch.arange(B, device=DEV)
+    r = _Route(rows, mask, I, k)
+    assert r.n_heavy == int(((lens > DENSE_MASK_MIN) & (lens <= I - k)).sum()) > 0
+    idx = r.topk(Q, items, k, float("-inf"), False)
+    ref, _ = ops.score_topk(Q, items, k, mask=mask)
+    S = Q.double() @ items.double().T
+    for u in range(B):
+        if lists[u]:
+            S[u, torch.tensor(lists[u], device=DEV)] = float("-inf")
+    kth = torch.topk(S, k, dim=1).values[:, -1:]
+    got = S.gather(1, idx.long())
+    heavy = torch.from_numpy((lens > DENSE_MASK_MIN) & (lens <= I - k)).to(DEV)
+    assert torch.isfinite(got[heavy]).all()
+    assert (got[heavy] >= (kth - 1e-5 * kth.abs().clamp(min=1.0))[heavy]).all()
+    assert torch.equal(idx[~heavy], ref[~heavy])  # the light users are the fused launch's own result
