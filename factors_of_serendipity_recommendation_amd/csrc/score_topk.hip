@@ -1686,10 +1686,33 @@ bool lds_eligible(int dtype, int64_t d, int k) {
            kLdsBytes;
 }
 
+SplitPlan plan_lds_splits(int64_t B, int64_t n_items, int dtype, int waves);
+
 SplitPlan plan_splits(int64_t B, int64_t n_items, int dtype, int64_t d, int k) {
     const int64_t tiles32 = ceil_div(n_items, 32);
     if (lds_eligible(dtype, d, k)) {
         const int waves = lds_waves(dtype, d, k);
+        if (dtype == LGX_DTYPE_F32 && waves == 8) {
+            // 256-user workgroups halve the user tiles: where that alone turns one catalog sweep into
+            // a split launch, the 4-wave walk without splits is faster (Gowalla shape, 27 522 users:
+            // 4 waves x 1 split 3.07 ms, 8 waves x 2 splits 3.20-3.23 ms unmasked top-20,
+            // profiles/r05_eval_shapes_ab_*.txt)
+            const SplitPlan p8 = plan_lds_splits(B, n_items, dtype, 8);
+            const SplitPlan p4 = plan_lds_splits(B, n_items, dtype, kF32LdsWaves);
+            return p8.n_splits > 1 && p4.n_splits == 1 ? p4 : p8;
+        }
+        return plan_lds_splits(B, n_items, dtype, waves);
+    }
+    const int64_t user_blocks = ceil_div(B, (int64_t)v1_waves(k) * kUsersPerWave);
+    int64_t s = ceil_div(2048, user_blocks);                       // aim for >= ~8 workgroups per CU
+    s = std::min<int64_t>(s, std::max<int64_t>(1, tiles32 / 8));  // >= 8 tiles per split
+    s = std::max<int64_t>(1, std::min<int64_t>(s, 64));
+    const int64_t per = ceil_div(tiles32, s) * 32;
+    return {(int)ceil_div(n_items, per), per, false, false, user_blocks, 0};
+}
+
+SplitPlan plan_lds_splits(int64_t B, int64_t n_items, int dtype, int waves) {
+    {
         const int64_t users = waves * kUsersPerWave, tile_items = kTileItems;
         const int64_t resident = lds_resident();
         const int64_t ut = ceil_div(B, users);
@@ -1698,15 +1721,18 @@ SplitPlan plan_splits(int64_t B, int64_t n_items, int dtype, int64_t d, int k) {
         // costs more than a partly filled last round (which plan_ranges moves to a split launch)
         if (ut >= resident) return {1, tiles * tile_items, true, false, ut, waves};
         // under one round: split the catalog.  Time ~ rounds / s * f(s): each split repeats the
-        // list-filling phase, measured +18 / +25 / +31 % per doubling of s from 2 to 16, i.e.
-        // log2 f = 0.12 L + 0.04 L^2 with L = log2 s.  Take the best s among 1-7 and multiples of 8
+        // list-filling phase, measured +18 / +25 / +31 % per doubling of s from 2 to 16 (bf16, C5
+        // catalog), i.e. log2 f = 0.12 L + 0.04 L^2 with L = log2 s.  fp32 at the evaluation shapes
+        // (catalogs of 40-90 K items, every tile of a split's start an event) pays more per split:
+        // log2 f = 0.25 L + 0.04 L^2 there.  Take the best s among 1-7 and multiples of 8
         // (XCD-affine), >= 4 tiles per split
+        const double a1 = dtype == LGX_DTYPE_F32 ? 0.25 : 0.12;
         int64_t s = 1;
         double best = 1e300;
         const int64_t s_max = std::max<int64_t>(1, std::min<int64_t>(256, tiles / 4));
         for (int64_t c = 1; c <= s_max; c = c < 8 ? c + 1 : c + 8) {
             const double L = std::log2((double)c);
-            const double t = (double)ceil_div(ut * c, resident) / (double)c * std::exp2(0.12 * L + 0.04 * L * L);
+            const double t = (double)ceil_div(ut * c, resident) / (double)c * std::exp2(a1 * L + 0.04 * L * L);
             if (t < best - 1e-12) {
                 best = t;
                 s = c;
@@ -1716,12 +1742,6 @@ SplitPlan plan_splits(int64_t B, int64_t n_items, int dtype, int64_t d, int k) {
         const int n = (int)ceil_div(n_items, per);
         return {n, per, true, n % 8 == 0, ut, waves};
     }
-    const int64_t user_blocks = ceil_div(B, (int64_t)v1_waves(k) * kUsersPerWave);
-    int64_t s = ceil_div(2048, user_blocks);                       // aim for >= ~8 workgroups per CU
-    s = std::min<int64_t>(s, std::max<int64_t>(1, tiles32 / 8));  // >= 8 tiles per split
-    s = std::max<int64_t>(1, std::min<int64_t>(s, 64));
-    const int64_t per = ceil_div(tiles32, s) * 32;
-    return {(int)ceil_div(n_items, per), per, false, false, user_blocks, 0};
 }
 
 template <typename KernelT>

@@ -157,6 +157,9 @@ class _Route:
         self.light_rows, self.heavy_rows = rows[self.light_pos].contiguous(), rows[self.heavy_pos].contiguous()
         self.light_mask = ops.csr_rows(mask, self.light_pos)
         self.heavy_mask = ops.csr_rows(mask, self.heavy_pos)
+        step = ops.dense_chunk_users(n_items)
+        self.heavy_offsets = [ops.dense_mask_offsets(self.heavy_mask, n_items, c0, min(self.n_heavy, c0 + step))
+                              for c0 in range(0, self.n_heavy, step)]
 
     def topk(self, users: torch.Tensor, items: torch.Tensor, k: int, mask_value: float, apply_sigmoid: bool):
         """idx int32 [n, k] for every user of the set, in set order."""
@@ -167,7 +170,8 @@ class _Route:
         if self.light_pos.numel():
             idx[self.light_pos] = ops.score_topk(users, items, k, user_rows=self.light_rows, mask=self.light_mask,
                                                  mask_value=mask_value, apply_sigmoid=apply_sigmoid)[0]
-        idx[self.heavy_pos] = ops.score_topk_dense_masked(users, items, k, self.heavy_rows, self.heavy_mask)
+        idx[self.heavy_pos] = ops.score_topk_dense_masked(users, items, k, self.heavy_rows, self.heavy_mask,
+                                                          offsets=self.heavy_offsets)
         return idx
 
 

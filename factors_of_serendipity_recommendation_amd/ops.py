@@ -268,26 +268,40 @@ def csr_rows(csr: Tuple[torch.Tensor, torch.Tensor], sel: torch.Tensor) -> Tuple
     return nip, ix[pos].contiguous()
 
 
+def dense_mask_offsets(mask: Tuple[torch.Tensor, torch.Tensor], n_items: int, c0: int, c1: int) -> torch.Tensor:
+    """Flat offsets (u - c0) * n_items + item of the masked entries of users [c0, c1) of a mask CSR:
+    where score_topk_dense_masked writes -inf into a [c1 - c0, n_items] score block."""
+    ip, ix = mask
+    sel = torch.arange(c0, c1, device=ip.device)
+    sp, sx = csr_rows(mask, sel)
+    rid = torch.repeat_interleave(torch.arange(c1 - c0, device=ip.device), sp[1:] - sp[:-1])
+    return rid * n_items + sx.to(torch.int64)
+
+
+def dense_chunk_users(n_items: int, chunk_bytes: int = 256 << 20) -> int:
+    return max(1, chunk_bytes // max(1, 4 * n_items))
+
+
 def score_topk_dense_masked(Q: torch.Tensor, items: torch.Tensor, k: int, user_rows: torch.Tensor,
-                            mask: Tuple[torch.Tensor, torch.Tensor], chunk_bytes: int = 256 << 20) -> torch.Tensor:
+                            mask: Tuple[torch.Tensor, torch.Tensor], chunk_bytes: int = 256 << 20,
+                            offsets: Optional[Sequence[torch.Tensor]] = None) -> torch.Tensor:
     """The ranking score_topk returns (idx int32 [B, k]; raw scores ranked, ties to the lower item id)
     by another route, for users whose mask is long: their dense raw score rows (lgx_score_dense), the
     masked entries set to -inf, the row top-k (lgx_topk_rows).  In the fused walk every masked item
     of such a user that reaches the running threshold needs an exact test (its 256-bit Bloom filter is
     saturated); here a mask costs one scattered store per item.  Every user must keep at least k
     unmasked items (the fused path's masked tail is not reproduced).  Users go in chunks of at most
-    chunk_bytes of scores."""
+    chunk_bytes of scores; offsets: the chunks' dense_mask_offsets, precomputed by a caller that ranks
+    the same users again (no host synchronisation then)."""
     require_gpu(Q, items, user_rows)
     B, I = user_rows.numel(), items.shape[0]
     idx = torch.empty((B, k), dtype=torch.int32, device=Q.device)
-    step = max(1, chunk_bytes // max(1, 4 * I))
-    for c0 in range(0, B, step):
+    step = dense_chunk_users(I, chunk_bytes)
+    for j, c0 in enumerate(range(0, B, step)):
         c1 = min(B, c0 + step)
-        sel = torch.arange(c0, c1, device=Q.device)
         S = score_dense(Q, items, user_rows=user_rows[c0:c1])
-        ip, ix = csr_rows(mask, sel)
-        rid = torch.repeat_interleave(torch.arange(c1 - c0, device=Q.device), ip[1:] - ip[:-1])
-        S.view(-1).index_fill_(0, rid * I + ix.to(torch.int64), float("-inf"))
+        off = offsets[j] if offsets is not None else dense_mask_offsets(mask, I, c0, c1)
+        S.view(-1).index_fill_(0, off, float("-inf"))
         idx[c0:c1] = topk_rows(S, k)[0]
         del S
     return idx

@@ -52,7 +52,7 @@ def _check(Q, items, idx, val, mask, sel, k, user_rows=None, chunk=250):
                                            (192, 7, True, 4), (256, 20, True, 4), (256, 21, False, 0),
                                            (96, 20, False, 0), (32, 20, False, 0)])
 def test_f32_kernel_selection(d, k, lds, waves):
-    plan = ops.score_topk_plan(40_000, 100_000, d, torch.float32, k)
+    plan = ops.score_topk_plan(65_536, 100_000, d, torch.float32, k)
     assert plan.startswith("score_topk_f32_lds") == lds, plan
     if lds:
         assert plan.startswith(f"score_topk_f32_lds<{waves} waves"), plan
@@ -69,6 +69,16 @@ def test_f32_split_mode(B, I, d, k, per):
     mask = _mask(B, I, per, g)
     idx, val = lgx.score_topk(Q, items, k, mask=mask)
     _check(Q, items, idx, val, mask, torch.arange(0, B, max(1, B // 600), device=DEV), k)
+
+
+def test_f32_eight_waves_only_where_they_do_not_split():
+    """d <= 128: 256-user workgroups, unless halving the user tiles alone would turn a single catalog
+    sweep into a split launch -- then the 4-wave walk without splits (the Gowalla shape)."""
+    assert ops.score_topk_plan(27_522, 40_981, 64, torch.float32, 20).startswith(
+        "score_topk_f32_lds<4 waves, 64-item tiles, 16x16x4> users[0,27522) full-sweep n_splits=1")
+    assert ops.score_topk_plan(52_643, 91_599, 128, torch.float32, 20).startswith(
+        "score_topk_f32_lds<8 waves, 64-item tiles, 16x16x4> users[0,52643) full-sweep n_splits=1")
+    assert ops.score_topk_plan(2_000, 50_000, 64, torch.float32, 20).startswith("score_topk_f32_lds<8 waves")
 
 
 @pytest.mark.parametrize("d,waves", [(256, 4), (128, 8), (64, 8)])
