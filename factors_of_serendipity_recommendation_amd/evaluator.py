@@ -127,27 +127,34 @@ def clear_caches() -> None:
     _BatchLists._cache.clear()
 
 
-# Users whose mask holds more than this many items are ranked by the dense route
+# Users whose mask holds more than dense_mask_min(n_items, d) items are ranked by the dense route
 # (ops.score_topk_dense_masked) when the catalog is small enough for dense rows (the evaluation
 # shapes): their 256-bit Bloom filter is saturated, so in the fused walk every one of their masked
 # items that reaches the running threshold takes an exact search.  On propagated LightGCN tables a
 # user's train items are among its best scores, and power-law users mask thousands of them
 # (tools/mask_probe.py, profiles/r05_mask_probe.txt: the ~5 % of Gowalla-shape users above 64 masked
-# items cost 1.6 ms of the 5.1 ms fused launch).
+# items cost 1.6 ms of the 5.1 ms fused launch).  A dense row costs about n_items * d, so the
+# threshold grows with it (tools/route_probe.py, profiles/r05_route_probe.txt: best near 64 at the
+# Gowalla shape, 256-1024 at the Amazon-book shape).
 DENSE_MASK_MIN = 64
 DENSE_MAX_ITEMS = 1 << 18
+
+
+def dense_mask_min(n_items: int, d: int) -> int:
+    return max(DENSE_MASK_MIN, n_items * d // 32768)
 
 
 class _Route:
     """The split of an evaluation set between the fused launch and the dense route."""
 
-    def __init__(self, rows: torch.Tensor, mask, n_items: int, k_max: int):
+    def __init__(self, rows: torch.Tensor, mask, n_items: int, k_max: int, d: int, thr: int = None):
         self.rows, self.mask = rows, mask
         n = rows.numel()
         lens = (mask[0][1:] - mask[0][:-1]) if mask is not None else None
         heavy = torch.zeros(n, dtype=torch.bool, device=rows.device)
+        self.thr = dense_mask_min(n_items, d) if thr is None else thr
         if lens is not None and n_items <= DENSE_MAX_ITEMS:
-            heavy = (lens > DENSE_MASK_MIN) & (lens <= n_items - k_max)
+            heavy = (lens > self.thr) & (lens <= n_items - k_max)
         self.n_heavy = int(heavy.sum())
         if self.n_heavy == 0:
             self.light_pos = None
@@ -203,10 +210,10 @@ class _TestLists:
         keys = np.repeat(np.arange(n, dtype=np.int64), self.recall_n) * self.M + flat
         self.keys = torch.unique(torch.from_numpy(keys).to(dev))  # sorted
 
-    def route(self, n_items: int, k: int) -> _Route:
-        key = (n_items, k)
+    def route(self, n_items: int, k: int, d: int) -> _Route:
+        key = (n_items, k, d)
         if key not in self.routes:
-            self.routes[key] = _Route(self.rows, self.mask, n_items, k)
+            self.routes[key] = _Route(self.rows, self.mask, n_items, k, d)
         return self.routes[key]
 
     def fingerprint(self, dataset) -> tuple:
@@ -249,7 +256,8 @@ def Test(dataset, Recmodel, epoch=0, w=None, multicore=0, topks: Sequence[int] =
     with torch.no_grad():
         all_users, all_items = Recmodel.computer()
         tl = _TestLists.get(dataset, all_items.shape[0], all_users.device)
-        idx = tl.route(all_items.shape[0], max_K).topk(all_users, all_items, max_K, -float(1 << 10), True)
+        idx = tl.route(all_items.shape[0], max_K, all_items.shape[1]).topk(all_users, all_items, max_K,
+                                                                          -float(1 << 10), True)
         res = _metrics_dev(tl.hit_mask(idx), tl.recall_n_dev, topks)
         for key in results:
             results[key] = res[key] / float(len(tl.users))
@@ -284,10 +292,10 @@ class _BatchLists:
         self.truth = ops.lists_to_device_csr(truths, dev, sort=False)
         self.routes: Dict[tuple, _Route] = {}
 
-    def route(self, n_items: int, k: int) -> _Route:
-        key = (n_items, k)
+    def route(self, n_items: int, k: int, d: int) -> _Route:
+        key = (n_items, k, d)
         if key not in self.routes:
-            self.routes[key] = _Route(self.rows, self.mask, n_items, k)
+            self.routes[key] = _Route(self.rows, self.mask, n_items, k, d)
         return self.routes[key]
 
     def fingerprint(self) -> tuple:
@@ -327,7 +335,8 @@ def batch_test(user_emb: torch.Tensor, item_emb: torch.Tensor, users_to_test: Se
     top_show = np.sort(np.asarray(Ks))
     max_top = int(max(top_show))
     bl = _BatchLists.get(users_to_test, train_items, test_set, train_set_flag, user_emb.device)
-    idx = bl.route(item_emb.shape[0], max_top).topk(user_emb, item_emb, max_top, float("-inf"), False)
+    idx = bl.route(item_emb.shape[0], max_top, item_emb.shape[1]).topk(user_emb, item_emb, max_top,
+                                                                       float("-inf"), False)
     curves = ops.foldout_metrics(idx, bl.truth)
     # the users' mean on the device: only 5 x max_top values cross to the host
     mean = ops.column_mean(curves).cpu().numpy()

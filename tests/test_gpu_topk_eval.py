@@ -196,22 +196,23 @@ def test_dense_masked_route_matches_float64(d):
 
 
 def test_evaluator_route_splits_long_masks():
-    """evaluator._Route: users with more than DENSE_MASK_MIN masked items (and at least k unmasked)
+    """evaluator._Route: users with more than dense_mask_min(I, d) masked items (and at least k unmasked)
     go to the dense route, the rest to the fused launch; both results land in set order and agree
     with the fused launch over everyone as top-k sets."""
-    from factors_of_serendipity_recommendation_amd.evaluator import DENSE_MASK_MIN, _Route
+    from factors_of_serendipity_recommendation_amd.evaluator import _Route, dense_mask_min
     g = torch.Generator(device=DEV).manual_seed(3)
     B, I, d, k = 2000, 30_000, 64, 20
     Q = torch.randn(B, d, device=DEV, generator=g) / 8
     items = torch.randn(I, d, device=DEV, generator=g) / 8
     rng = np.random.default_rng(3)
-    lens = np.where(rng.random(B) < 0.1, rng.integers(DENSE_MASK_MIN + 1, 5000, B), rng.integers(0, 40, B))
+    thr = dense_mask_min(I, d)
+    lens = np.where(rng.random(B) < 0.1, rng.integers(thr + 1, 5000, B), rng.integers(0, 40, B))
     lens[7] = I - k + 1  # fewer than k unmasked items: stays on the fused path (its masked tail)
     lists = [sorted(rng.choice(I, int(n), replace=False).tolist()) for n in lens]
     mask = ops.lists_to_device_csr(lists, DEV)
     rows = torch.arange(B, device=DEV)
-    r = _Route(rows, mask, I, k)
-    assert r.n_heavy == int(((lens > DENSE_MASK_MIN) & (lens <= I - k)).sum()) > 0
+    r = _Route(rows, mask, I, k, d)
+    assert r.thr == thr and r.n_heavy == int(((lens > thr) & (lens <= I - k)).sum()) > 0
     idx = r.topk(Q, items, k, float("-inf"), False)
     ref, _ = ops.score_topk(Q, items, k, mask=mask)
     S = Q.double() @ items.double().T
@@ -220,7 +221,7 @@ def test_evaluator_route_splits_long_masks():
             S[u, torch.tensor(lists[u], device=DEV)] = float("-inf")
     kth = torch.topk(S, k, dim=1).values[:, -1:]
     got = S.gather(1, idx.long())
-    heavy = torch.from_numpy((lens > DENSE_MASK_MIN) & (lens <= I - k)).to(DEV)
+    heavy = torch.from_numpy((lens > thr) & (lens <= I - k)).to(DEV)
     assert torch.isfinite(got[heavy]).all()
     assert (got[heavy] >= (kth - 1e-5 * kth.abs().clamp(min=1.0))[heavy]).all()
     assert torch.equal(idx[~heavy], ref[~heavy])  # the light users are the fused launch's own result

@@ -491,7 +491,7 @@ def row_eval(rows, reps, tmpdir, cfg_name):
         t1 = sync_t()
         tl = evaluator._TestLists.get(ds, all_items.shape[0], all_users.device)
         t2 = sync_t()
-        idx = tl.route(all_items.shape[0], 20).topk(all_users, all_items, 20, -float(1 << 10), True)
+        idx = tl.route(all_items.shape[0], 20, cfg.d).topk(all_users, all_items, 20, -float(1 << 10), True)
         t3 = sync_t()
         evaluator._metrics_dev(tl.hit_mask(idx), tl.recall_n_dev, [20])
         t4 = sync_t()
@@ -530,13 +530,13 @@ def row_eval(rows, reps, tmpdir, cfg_name):
            f"recall@20 {float(res['recall'][0]):.5f} (synthetic graph)")
     # the score + mask + top-20 step inside the loop (the fused launch for most users, the dense route
     # for users with long masks), against the f32 MFMA peak (its own HIP-event timing)
-    rt = tl.route(all_items.shape[0], 20)
+    rt = tl.route(all_items.shape[0], 20, cfg.d)
     ms_k = gpu_ms(lambda: rt.topk(all_users, all_items, 20, -float(1 << 10), True), reps)
     fl = 2.0 * n_test * cfg.n_items * cfg.d
     n_light = n_test - rt.n_heavy
     plan = ops.score_topk_plan(n_light, cfg.n_items, cfg.d, torch.float32, 20)
     rows[-1]["roofline"] = {"bound": "mfma_f32", "kernel": plan + f"; {rt.n_heavy} users with > "
-                            f"{evaluator.DENSE_MASK_MIN} masked items by the dense route (score_dense_lds + "
+                            f"{rt.thr} masked items by the dense route (score_dense_lds + "
                             "topk_rows_kernel)", "launch_ms": ms_k,
                             "achieved": fl / (ms_k / 1e3) / 1e12, "peak": F32_PEAK / 1e12, "unit": "TFLOP/s",
                             "frac": fl / (ms_k / 1e3) / F32_PEAK,
@@ -562,7 +562,7 @@ def row_eval(rows, reps, tmpdir, cfg_name):
         t0 = sync_t()
         bl = evaluator._BatchLists.get(users, train_items, test_set, 0, all_users.device)
         t1 = sync_t()
-        bidx = bl.route(all_items.shape[0], 20).topk(all_users, all_items, 20, float("-inf"), False)
+        bidx = bl.route(all_items.shape[0], 20, cfg.d).topk(all_users, all_items, 20, float("-inf"), False)
         t2 = sync_t()
         curves = ops.foldout_metrics(bidx, bl.truth)
         t3 = sync_t()
@@ -571,7 +571,7 @@ def row_eval(rows, reps, tmpdir, cfg_name):
         for k_, a_, b_ in (("lists", t0, t1), ("score_topk", t1, t2), ("foldout", t2, t3), ("mean", t3, t4)):
             bph[k_].append((b_ - a_) * 1e3)
     bph = {k_: float(np.median(v)) for k_, v in bph.items()}
-    brt = bl.route(all_items.shape[0], 20)
+    brt = bl.route(all_items.shape[0], 20, cfg.d)
     ms_bk = gpu_ms(lambda: brt.topk(all_users, all_items, 20, float("-inf"), False), reps)
     Eu_h, Ei_h = all_users.float().cpu(), all_items.float().cpu()
     bu = users[:1024]

@@ -54,9 +54,8 @@ with tempfile.TemporaryDirectory() as tmp:
                                              apply_sigmoid=True))
         print(f"{name}: {n} test users, all fused: {fused:.2f} ms  [{ops.score_topk_plan(n, I.shape[0], cfg.d, torch.float32, 20)}]",
               flush=True)
-        for thr in (32, 64, 128, 256, 1024):
-            evaluator.DENSE_MASK_MIN = thr
-            r = evaluator._Route(tl.rows, tl.mask, I.shape[0], 20)
+        for thr in (32, 64, 128, 256, 1024, None):
+            r = evaluator._Route(tl.rows, tl.mask, I.shape[0], 20, cfg.d, thr)
             tot = timed(lambda: r.topk(U, I, 20, -1024.0, True))
             if r.n_heavy:
                 tf = timed(lambda: ops.score_topk(U, I, 20, user_rows=r.light_rows, mask=r.light_mask,
@@ -66,8 +65,7 @@ with tempfile.TemporaryDirectory() as tmp:
                 plan = ops.score_topk_plan(n - r.n_heavy, I.shape[0], cfg.d, torch.float32, 20)
             else:
                 tf, td, plan = tot, 0.0, "-"
-            print(f"   threshold {thr}: {r.n_heavy} dense users, route {tot:.2f} ms = fused {tf:.2f} + dense {td:.2f}  [{plan}]",
+            print(f"   threshold {r.thr}{' (the rule)' if thr is None else ''}: {r.n_heavy} dense users, route {tot:.2f} ms = fused {tf:.2f} + dense {td:.2f}  [{plan}]",
                   flush=True)
-        evaluator.DENSE_MASK_MIN = 64
         del model, ds
         torch.cuda.empty_cache()
