@@ -1,0 +1,115 @@
+"""Development: build a cycle-stamped copy of liblgx.so (tools/_ab/lab/liblgx.so) for
+tools/score_stats.py.  The LDS scoring walk (score_topk_lds_body) gets s_memtime stamps around its
+phases and counters on its epilogue paths, summed per wave into a device array read back by
+lgx_lab_stats().  The product sources are copied and patched here, never edited: the product
+library has no lab switches.  Stamping costs ~10 % of wave cycles (MI355X_MICROARCH.md); the
+numbers are a breakdown, not a timing.
+
+  python tools/make_stats_lab.py        # then: python tools/score_stats.py
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LAB = os.path.join(ROOT, "tools", "_ab", "lab")
+
+# [index, name] of the per-wave sums (tools/score_stats.py reads the same list)
+FIELDS = ["waves", "tiles", "cyc_loop", "cyc_stage", "cyc_epi_late", "cyc_compute", "cyc_epi_early", "cyc_wait",
+          "n_fast", "n_defer", "n_full", "cyc_full", "cyc_flush", "n_event_tiles"]
+
+
+def patch(src: str) -> str:
+    def rep(old, new, count=1):
+        nonlocal src
+        assert src.count(old) >= 1, old[:80]
+        src = src.replace(old, new, count)
+
+    # device sums + host accessor
+    rep("namespace lgx {\nnamespace {\n", "namespace lgx {\n__device__ unsigned long long g_lab[32];\nnamespace {\n")
+    # per-wave accumulators at the loop
+    rep("    const bool stage_after = STAGGER && !late;  // wave-uniform\n    for (int64_t t = 0; t < ntiles; ++t) {\n"
+        "        const int64_t t0 = tile_start(t);\n"
+        "        if (!stage_after && t + ahead < ntiles) stage(sbuf, tile_start(t + ahead));\n"
+        "        if (late && t > 0) epilogue(prev_t0);\n"
+        "        compute();\n"
+        "        if (stage_after && t + ahead < ntiles) stage(sbuf, tile_start(t + ahead));\n"
+        "        if (!late) epilogue(t0);\n",
+        "    const bool stage_after = STAGGER && !late;  // wave-uniform\n"
+        "    unsigned long long L_loop0 = __builtin_amdgcn_s_memtime();\n"
+        "    for (int64_t t = 0; t < ntiles; ++t) {\n"
+        "        const int64_t t0 = tile_start(t);\n"
+        "        const unsigned long long T0 = __builtin_amdgcn_s_memtime();\n"
+        "        if (!stage_after && t + ahead < ntiles) stage(sbuf, tile_start(t + ahead));\n"
+        "        const unsigned long long T1 = __builtin_amdgcn_s_memtime();\n"
+        "        if (late && t > 0) epilogue(prev_t0);\n"
+        "        const unsigned long long T2 = __builtin_amdgcn_s_memtime();\n"
+        "        compute();\n"
+        "        const unsigned long long T3 = __builtin_amdgcn_s_memtime();\n"
+        "        if (stage_after && t + ahead < ntiles) stage(sbuf, tile_start(t + ahead));\n"
+        "        const unsigned long long T4 = __builtin_amdgcn_s_memtime();\n"
+        "        if (!late) epilogue(t0);\n"
+        "        const unsigned long long T5 = __builtin_amdgcn_s_memtime();\n"
+        "        L_stage += (T1 - T0) + (T4 - T3); L_epi_late += T2 - T1; L_compute += T3 - T2; L_epi_early += T5 - T4;\n")
+    rep("        __syncthreads();\n        buf = buf + 1 == nbuf ? 0 : buf + 1;\n",
+        "        __syncthreads();\n        L_wait += __builtin_amdgcn_s_memtime() - T5;\n        ++L_tiles;\n"
+        "        buf = buf + 1 == nbuf ? 0 : buf + 1;\n")
+    rep("    if (late && ntiles > 0) epilogue(prev_t0);\n",
+        "    if (late && ntiles > 0) epilogue(prev_t0);\n"
+        "    const unsigned long long L_loop = __builtin_amdgcn_s_memtime() - L_loop0;\n")
+    # declarations before the epilogue lambda
+    rep("    auto epilogue = [&](int64_t e0) {\n",
+        "    unsigned long long L_stage = 0, L_epi_late = 0, L_compute = 0, L_epi_early = 0, L_wait = 0, L_tiles = 0;\n"
+        "    unsigned long long L_fast = 0, L_defer = 0, L_full = 0, L_cyc_full = 0, L_ev = 0;\n"
+        "    auto epilogue = [&](int64_t e0) {\n")
+    rep("                if (__ballot((m0 >= tauA) | (m1 >= tauB)) == 0ull) return;  // wave-uniform fast path\n",
+        "                if (__ballot((m0 >= tauA) | (m1 >= tauB)) == 0ull) { ++L_fast; return; }  // wave-uniform fast path\n"
+        "                ++L_ev;\n")
+    rep("                    if (__ballot(n > TopK::kPend) == 0ull) {\n                        st.pcnt = n;\n"
+        "                        return;\n                    }\n",
+        "                    if (__ballot(n > TopK::kPend) == 0ull) {\n                        st.pcnt = n;\n"
+        "                        ++L_defer;\n                        return;\n                    }\n")
+    rep("        const float tau_before = st.tau;\n",
+        "        const unsigned long long F0 = __builtin_amdgcn_s_memtime();\n        ++L_full;\n"
+        "        const float tau_before = st.tau;\n")
+    rep("        if (SKIP && __ballot(st.tau != tau_before) != 0ull) refresh_taus();\n    };\n",
+        "        if (SKIP && __ballot(st.tau != tau_before) != 0ull) refresh_taus();\n"
+        "        L_cyc_full += __builtin_amdgcn_s_memtime() - F0;\n    };\n")
+    # the sums, then the flush (top-k mode only)
+    rep("    st.flush(a, split, lane);\n}\n\ntemplate <int KSTEPS, bool MINMAX, int MODE = kTopK>",
+        "    const unsigned long long FL0 = __builtin_amdgcn_s_memtime();\n"
+        "    st.flush(a, split, lane);\n"
+        "    const unsigned long long L_flush = __builtin_amdgcn_s_memtime() - FL0;\n"
+        "    if (lane == 0) {\n"
+        "        const unsigned long long v[14] = {1ull, L_tiles, L_loop, L_stage, L_epi_late, L_compute, L_epi_early,\n"
+        "                                          L_wait, L_fast, L_defer, L_full, L_cyc_full, L_flush, L_ev};\n"
+        "        for (int j = 0; j < 14; ++j) atomicAdd(&g_lab[j], v[j]);\n"
+        "    }\n"
+        "}\n\ntemplate <int KSTEPS, bool MINMAX, int MODE = kTopK>")
+    src += ("\nextern \"C\" int lgx_lab_stats(unsigned long long* out, int reset) {\n"
+            "    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lgx::g_lab), sizeof(lgx::g_lab)) != hipSuccess) return 1;\n"
+            "    if (reset) {\n        unsigned long long z[32] = {0};\n"
+            "        if (hipMemcpyToSymbol(HIP_SYMBOL(lgx::g_lab), z, sizeof(z)) != hipSuccess) return 1;\n    }\n"
+            "    return 0;\n}\n")
+    return src
+
+
+def main():
+    if os.path.isdir(LAB):
+        shutil.rmtree(LAB)
+    pkg = os.path.join(LAB, "factors_of_serendipity_recommendation_amd")
+    shutil.copytree(os.path.join(ROOT, "factors_of_serendipity_recommendation_amd", "csrc"), os.path.join(pkg, "csrc"),
+                    ignore=shutil.ignore_patterns("_build"))
+    shutil.copytree(os.path.join(ROOT, "include"), os.path.join(LAB, "include"))
+    p = os.path.join(pkg, "csrc", "score_topk.hip")
+    with open(p) as f:
+        src = f.read()
+    with open(p, "w") as f:
+        f.write(patch(src))
+    subprocess.check_call(["make", "-s", f"-j{min(8, os.cpu_count() or 8)}", "-C", os.path.join(pkg, "csrc")])
+    print(os.path.join(pkg, "liblgx.so"))
+
+
+if __name__ == "__main__":
+    sys.exit(main())
