@@ -17,7 +17,7 @@ LAB = os.path.join(ROOT, "tools", "_ab", "lab")
 
 # [index, name] of the per-wave sums (tools/score_stats.py reads the same list)
 FIELDS = ["waves", "tiles", "cyc_loop", "cyc_stage", "cyc_epi_late", "cyc_compute", "cyc_epi_early", "cyc_wait",
-          "n_fast", "n_defer", "n_full", "cyc_full", "cyc_flush", "n_event_tiles"]
+          "n_fast", "n_defer", "n_full", "cyc_full", "cyc_flush", "n_event_tiles", "cyc_detect", "cyc_defer"]
 
 
 def patch(src: str) -> str:
@@ -61,15 +61,22 @@ def patch(src: str) -> str:
     # declarations before the epilogue lambda
     rep("    auto epilogue = [&](int64_t e0) {\n",
         "    unsigned long long L_stage = 0, L_epi_late = 0, L_compute = 0, L_epi_early = 0, L_wait = 0, L_tiles = 0;\n"
-        "    unsigned long long L_fast = 0, L_defer = 0, L_full = 0, L_cyc_full = 0, L_ev = 0;\n"
+        "    unsigned long long L_fast = 0, L_defer = 0, L_full = 0, L_cyc_full = 0, L_ev = 0, L_detect = 0, L_defer_cyc = 0;\n"
         "    auto epilogue = [&](int64_t e0) {\n")
+    rep("        const bool tail = e0 + G::TILE_ITEMS > i_end;\n        if constexpr (SKIP) {\n",
+        "        const bool tail = e0 + G::TILE_ITEMS > i_end;\n        const unsigned long long E0 = __builtin_amdgcn_s_memtime();\n"
+        "        if constexpr (SKIP) {\n")
     rep("                if (__ballot((m0 >= tauA) | (m1 >= tauB)) == 0ull) return;  // wave-uniform fast path\n",
-        "                if (__ballot((m0 >= tauA) | (m1 >= tauB)) == 0ull) { ++L_fast; return; }  // wave-uniform fast path\n"
+        "                const bool any_ev = __ballot((m0 >= tauA) | (m1 >= tauB)) != 0ull;\n"
+        "                const unsigned long long E1 = __builtin_amdgcn_s_memtime();\n"
+        "                L_detect += E1 - E0;\n"
+        "                if (!any_ev) { ++L_fast; return; }  // wave-uniform fast path\n"
         "                ++L_ev;\n")
     rep("                    if (__ballot(n > TopK::kPend) == 0ull) {\n                        st.pcnt = n;\n"
         "                        return;\n                    }\n",
         "                    if (__ballot(n > TopK::kPend) == 0ull) {\n                        st.pcnt = n;\n"
-        "                        ++L_defer;\n                        return;\n                    }\n")
+        "                        ++L_defer;\n                        L_defer_cyc += __builtin_amdgcn_s_memtime() - E1;\n"
+        "                        return;\n                    }\n")
     rep("        const float tau_before = st.tau;\n",
         "        const unsigned long long F0 = __builtin_amdgcn_s_memtime();\n        ++L_full;\n"
         "        const float tau_before = st.tau;\n")
@@ -82,9 +89,10 @@ def patch(src: str) -> str:
         "    st.flush(a, split, lane);\n"
         "    const unsigned long long L_flush = __builtin_amdgcn_s_memtime() - FL0;\n"
         "    if (lane == 0) {\n"
-        "        const unsigned long long v[14] = {1ull, L_tiles, L_loop, L_stage, L_epi_late, L_compute, L_epi_early,\n"
-        "                                          L_wait, L_fast, L_defer, L_full, L_cyc_full, L_flush, L_ev};\n"
-        "        for (int j = 0; j < 14; ++j) atomicAdd(&g_lab[j], v[j]);\n"
+        "        const unsigned long long v[16] = {1ull, L_tiles, L_loop, L_stage, L_epi_late, L_compute, L_epi_early,\n"
+        "                                          L_wait, L_fast, L_defer, L_full, L_cyc_full, L_flush, L_ev, L_detect,\n"
+        "                                          L_defer_cyc};\n"
+        "        for (int j = 0; j < 16; ++j) atomicAdd(&g_lab[j], v[j]);\n"
         "    }\n"
         "}\n\ntemplate <int KSTEPS, bool MINMAX, int MODE = kTopK>")
     src += ("\nextern \"C\" int lgx_lab_stats(unsigned long long* out, int reset) {\n"

@@ -48,10 +48,13 @@ def stats(fn, label):
     per = {k: v[k] / wt for k in ("cyc_loop", "cyc_stage", "cyc_epi_late", "cyc_compute", "cyc_epi_early", "cyc_wait")}
     frac = {k: v[k] / wt for k in ("n_fast", "n_event_tiles", "n_defer", "n_full")}
     full_cyc = v["cyc_full"] / max(1, v["n_full"])
+    det = v["cyc_detect"] / wt
+    dfr = v["cyc_defer"] / max(1, v["n_defer"])
     print(f"{label}: {e0.elapsed_time(e1):.2f} ms (stamped), {v['waves']} waves, {v['tiles'] / max(1, v['waves']):.0f} tiles/wave", flush=True)
     print("   cycles per wave-tile: " + ", ".join(f"{k[4:]} {x:.0f}" for k, x in per.items()), flush=True)
     print("   per wave-tile: " + ", ".join(f"{k[2:]} {x:.3f}" for k, x in frac.items())
-          + f"; cycles per full path {full_cyc:.0f}; flush {v['cyc_flush'] / max(1, v['waves']):.0f} per wave", flush=True)
+          + f"; cycles per full path {full_cyc:.0f}; flush {v['cyc_flush'] / max(1, v['waves']):.0f} per wave; "
+            f"detect (incl. the MFMA results' wait) {det:.0f} per wave-tile; deferred path {dfr:.0f} per deferral", flush=True)
 
 
 if ONLY in (None, "eval"):
