@@ -1823,13 +1823,7 @@ int launch_f32_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t st
 template <bool MM, int MODE = kTopK>
 int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream, int dtype = LGX_DTYPE_BF16) {
     const int ksteps = (int)(a.d / 16);
-    if constexpr (MODE == kFloorOnly) {
-        if (dtype == LGX_DTYPE_F32) {
-            set_error("lgx_score_topk: score floors are a bf16 LDS kernel mode");
-            return LGX_ERR_UNSUPPORTED;
-        }
-    }
-    if constexpr (MODE != kFloorOnly) {
+    {
         if (dtype == LGX_DTYPE_F32) {
             if (p.waves == 8) {
                 switch (ksteps) {
@@ -1930,12 +1924,24 @@ inline bool seeded_sweep(const SplitPlan& p, bool minmax, int64_t n_items) {
 // 1M items, d=256 bf16, masked (profiles/r03_score_lab_stageprof.txt, r03_score_lab_floor.txt): the
 // first stage [0, 16384) 5.10 ms, of which 4.24 ms events; with floors over its first 2048 / 4096 /
 // 8192 / 16384 items (the pass included) 4.26 / 3.78 / 3.30 / 2.87 ms, all 7 stages 57.84 ->
-// 54.40 ms at 16384, lists identical.  Splits shorter than 4 x kFloorItems go without, and so does
-// fp32: at 1/16 of the bf16 MFMA rate its events are cheap beside its tiles, and the pass cost more
-// than it saved (bench fp32 leg 1044 -> 1052 ms with floors; bf16 leg 432 -> 418 ms).
+// 54.40 ms at 16384, lists identical.  Splits shorter than 4 x kFloorItems go without.
+// fp32: at the C5 catalog (seeded stages) its events are cheap beside its 16x slower tiles and the
+// pass cost more than it saved (bench fp32 leg 1044 -> 1052 ms with floors).  At the evaluation
+// shapes (catalogs under 262 144 items, no seeded stages) the one-wave-per-SIMD walk (4 waves) has
+// no partner wave to hide its events under, and a streaming top-k meets most of its ~k ln(n / k)
+// insertions early: there the floor over each split's first eighth pays (Gowalla shape, propagated
+// tables, the route's fused part 3.25 -> 2.89 ms; profiles/r05_eval_variants.txt).  The 8-wave walk
+// hides its events under the partner's MFMAs and gained nothing (Amazon-book shape 14.95 -> 15.08 ms),
+// nor did top-1 (few events: 1.89 -> 1.96 ms).
 constexpr int64_t kFloorItems = 16384;
-inline bool floored(const SplitPlan& p, bool minmax, int dtype) {
-    return p.lds && !minmax && dtype == LGX_DTYPE_BF16 && p.split_items >= 4 * kFloorItems;
+constexpr int64_t kF32FloorMinSplit = 4096;
+inline int64_t floor_items_for(const SplitPlan& p, int dtype, int64_t n_items, int k) {
+    if (dtype == LGX_DTYPE_BF16) return p.split_items >= 4 * kFloorItems ? kFloorItems : 0;
+    if (p.waves != kF32LdsWaves || k < 8 || n_items >= 16 * kSeedItems || p.split_items < kF32FloorMinSplit) return 0;
+    return ceil_div(ceil_div(p.split_items, 8), (int64_t)kTileItems) * kTileItems;
+}
+inline bool floored(const SplitPlan& p, bool minmax, int dtype, int64_t n_items, int k) {
+    return p.lds && !minmax && floor_items_for(p, dtype, n_items, k) > 0;
 }
 
 size_t topk_ws_bytes(int64_t B, int64_t n_items, int k, int dtype, int64_t d) {
@@ -1977,9 +1983,10 @@ extern "C" int lgx_score_topk_plan(int64_t B, int64_t n_items, int64_t d, int dt
                                  : (v1_waves(k) == 4 ? "score_topk_kernel<4 waves>" : "score_topk_kernel<1 wave>");
         const char* mode = p.lds ? (p.n_splits == 1 ? "full-sweep" : (p.xcd_affine ? "split-xcd" : "split"))
                                  : "split";
-        off += snprintf(buf + off, len - off, "%s%s users[%lld,%lld) %s%s n_splits=%d utiles=%lld",
+        off += snprintf(buf + off, len - off, "%s%s users[%lld,%lld) %s%s%s n_splits=%d utiles=%lld",
                         i ? "; " : "", kern, (long long)r[i].u0, (long long)r[i].u1, mode,
-                        seeded_sweep(p, false, n_items) ? " (seeded in stages)" : "", p.n_splits,
+                        seeded_sweep(p, false, n_items) ? " (seeded in stages)" : "",
+                        floored(p, false, dtype, n_items, k) ? " (score floors)" : "", p.n_splits,
                         (long long)p.n_utiles);
     }
     return LGX_OK;
@@ -2025,9 +2032,9 @@ extern "C" int lgx_score_topk(const void* Q, const int64_t* user_rows, const voi
                     reinterpret_cast<float*>(wsr), reinterpret_cast<int32_t*>(wsr + list_bytes), minmax,
                     range_susp_bytes(R) ? reinterpret_cast<uint64_t*>(wsr + 2 * list_bytes) : nullptr};
         int rc;
-        if (floored(p, mm, dtype)) {  // the floors of every split's first kFloorItems items, then the sweep reads them
+        if (floored(p, mm, dtype, n_items, k)) {  // every split's floor over its first items; the sweep reads them
             a.floor = reinterpret_cast<float*>(wsr + 2 * list_bytes + range_susp_bytes(R));
-            a.floor_items = kFloorItems;
+            a.floor_items = floor_items_for(p, dtype, n_items, k);
             rc = launch_lds<false, kFloorOnly>(a, p, stream, dtype);
             if (rc) return rc;
         }

@@ -205,7 +205,7 @@ def test_score_topk_plan_seeds_large_full_sweeps():
     import torch
     from factors_of_serendipity_recommendation_amd import ops
     big = ops.score_topk_plan(1_000_000, 1_000_000, 256, torch.bfloat16, 20)
-    assert big.split("; ")[0].endswith("full-sweep (seeded in stages) n_splits=1 utiles=3840"), big
+    assert big.split("; ")[0].endswith("full-sweep (seeded in stages) (score floors) n_splits=1 utiles=3840"), big
     assert "seeded" not in big.split("; ")[1]
     assert "seeded" in ops.score_topk_plan(65536, 262_144, 256, torch.bfloat16, 20)
     assert "seeded" not in ops.score_topk_plan(65536, 262_143, 256, torch.bfloat16, 20)

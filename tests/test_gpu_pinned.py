@@ -262,6 +262,43 @@ def test_score_floors_with_ties_and_masked_group_maxima(mode, dtype):
     assert not torch.isin(got, users * I + mask[1].long()).any(), "a masked item was returned"
 
 
+@pytest.mark.parametrize("B,I,d", [(27_522, 40_981, 64), (3_000, 100_000, 256), (2_000, 100_000, 192)])
+def test_f32_score_floors_at_evaluation_shapes(B, I, d):
+    """fp32 score floors (the 4-wave walk, catalogs under 262 144 items: the evaluation shapes of
+    Procedure.Test / batch_test): every split takes its floor over its first eighth.  The catalog repeats
+    2048 distinct rows, so a user's best scores come in exact ties spread over many floor groups, and the
+    mask takes out every copy of the user's best row plus random items.  Lists equal, as sets with their
+    values, the unfloored sweep of the min/max variant; no masked item comes back."""
+    k = 20
+    plan = ops.score_topk_plan(B, I, d, torch.float32, k)
+    assert plan.startswith("score_topk_f32_lds<4 waves") and "(score floors)" in plan, plan
+    g = torch.Generator(device=DEV).manual_seed(B + d)
+    Q = torch.randn(B, d, device=DEV, generator=g) / 8
+    base = torch.randn(2048, d, device=DEV, generator=g) / 8
+    rowid = torch.randint(0, 2048, (I,), device=DEV, generator=g)
+    items = base[rowid].contiguous()
+    best = torch.cat([(Q[u0:u0 + 4096] @ base.T).argmax(1) for u0 in range(0, B, 4096)])
+    order = torch.argsort(rowid)
+    srt = rowid[order]
+    s0, s1 = torch.searchsorted(srt, best), torch.searchsorted(srt, best, right=True)
+    j = s0[:, None] + torch.arange(int((s1 - s0).max()), device=DEV)[None, :]
+    copies = torch.where(j < s1[:, None], order[j.clamp(max=I - 1)], -1)
+    m = torch.cat([copies, torch.randint(0, I, (B, 25), device=DEV, generator=g)], 1).sort(1).values
+    keep = m >= 0
+    keep[:, 1:] &= m[:, 1:] != m[:, :-1]
+    indptr = torch.zeros(B + 1, dtype=torch.int64, device=DEV)
+    indptr[1:] = torch.cumsum(keep.sum(1), 0)
+    mask = (indptr, m[keep].to(torch.int32))
+    idx, val = lgx.score_topk(Q, items, k, mask=mask)
+    idx1, val1, _ = lgx.score_topk(Q, items, k, mask=mask, want_minmax=True)
+    ka, kb = torch.sort(idx.long(), 1), torch.sort(idx1.long(), 1)
+    assert torch.equal(ka.values, kb.values), "floored lists differ from the unfloored sweep"
+    assert torch.equal(val.gather(1, ka.indices), val1.gather(1, kb.indices))
+    users = torch.repeat_interleave(torch.arange(B, device=DEV), indptr[1:] - indptr[:-1])
+    got = torch.arange(B, device=DEV)[:, None] * I + idx.long()
+    assert not torch.isin(got, users * I + mask[1].long()).any(), "a masked item was returned"
+
+
 @pytest.mark.parametrize("d,k,rows", [(64, 1, False), (128, 7, True), (128, 32, False), (256, 20, True),
                                       (96, 20, True)])
 def test_seeded_sweep_shapes(d, k, rows):

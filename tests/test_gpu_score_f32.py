@@ -74,10 +74,11 @@ def test_f32_split_mode(B, I, d, k, per):
 def test_f32_eight_waves_only_where_they_do_not_split():
     """d <= 128: 256-user workgroups, unless halving the user tiles alone would turn a single catalog
     sweep into a split launch -- then the 4-wave walk without splits (the Gowalla shape)."""
-    assert ops.score_topk_plan(27_522, 40_981, 64, torch.float32, 20).startswith(
-        "score_topk_f32_lds<4 waves, 64-item tiles, 16x16x4> users[0,27522) full-sweep n_splits=1")
-    assert ops.score_topk_plan(52_643, 91_599, 128, torch.float32, 20).startswith(
-        "score_topk_f32_lds<8 waves, 64-item tiles, 16x16x4> users[0,52643) full-sweep n_splits=1")
+    gow = ops.score_topk_plan(27_522, 40_981, 64, torch.float32, 20)
+    assert gow.startswith("score_topk_f32_lds<4 waves, 64-item tiles, 16x16x4> users[0,27522) full-sweep") and \
+        "n_splits=1" in gow and ";" not in gow, gow
+    amz = ops.score_topk_plan(52_643, 91_599, 128, torch.float32, 20)
+    assert amz == "score_topk_f32_lds<8 waves, 64-item tiles, 16x16x4> users[0,52643) full-sweep n_splits=1 utiles=206", amz
     assert ops.score_topk_plan(2_000, 50_000, 64, torch.float32, 20).startswith("score_topk_f32_lds<8 waves")
 
 
