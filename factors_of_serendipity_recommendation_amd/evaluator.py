@@ -289,7 +289,9 @@ class _BatchLists:
         else:
             truths = [train_items[u] for u in ul]
             self.mask = None
-        self.truth = ops.lists_to_device_csr(truths, dev, sort=False)
+        # sorted (the fold-out curves treat a truth list as a set; lgx_foldout_metrics binary-searches
+        # long sorted lists)
+        self.truth = ops.lists_to_device_csr(truths, dev, sort=True)
         self.routes: Dict[tuple, _Route] = {}
 
     def route(self, n_items: int, k: int, d: int) -> _Route:

@@ -732,3 +732,23 @@ def test_column_mean_is_numpy_mean_bit_for_bit(rows, cols):
             want = np.mean(a, axis=0)
     assert want.dtype == np.float32
     assert np.array_equal(got, want, equal_nan=True)
+
+
+@pytest.mark.parametrize("k,sort", [(5, True), (20, True), (20, False), (32, True), (64, True)])
+def test_foldout_metrics_long_truth_lists(k, sort):
+    """Power-law truth lists (17..3000 items, duplicates included) on both long-list paths of
+    lgx_foldout_metrics -- the per-rank binary search of a sorted list and the streamed compare of an
+    unsorted one (and the plain scan for k > 32) -- bit-exact vs the oracle."""
+    rng = np.random.default_rng(k + 7 * sort)
+    users, n_items = 700, 20_000
+    rankings = np.stack([rng.permutation(n_items)[:k] for _ in range(users)]).astype(np.int32)
+    lens = np.minimum(3000, (17 + rng.pareto(1.2, users) * 40).astype(np.int64))
+    truths = []
+    for u in range(users):
+        t = list(rng.choice(n_items, size=int(lens[u]), replace=False))
+        t += list(rankings[u, :3]) if u % 5 == 0 else []     # hits at the top ranks
+        t += t[:2] if u % 7 == 0 else []                      # duplicates
+        truths.append(sorted(t) if sort else t)
+    rankings[3, :] = -1  # a ranking shorter than k (catalog < k): -1 never hits
+    got = ops.foldout_metrics(torch.from_numpy(rankings).to(DEV), ops.lists_to_device_csr(truths, DEV, sort=False))
+    assert np.array_equal(got.cpu().numpy(), oracle.evaluate_foldout(rankings, truths))
