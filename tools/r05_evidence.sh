@@ -14,5 +14,3 @@ cat $OUT/smoke.txt
 bash tools/profile_round.sh r05 > $OUT/profile.txt 2>&1 || { tail -20 $OUT/profile.txt; exit 1; }
 tail -2 $OUT/profile.txt
 head -c 1500 gpurun_out/prof_r05/bench_with_traffic.json
-timeout -k 10 900 python -u tools/bench_rows.py --out $OUT/rows.json > $OUT/rows.log 2>&1 || { tail -30 $OUT/rows.log; exit 1; }
-echo rows ok
