@@ -17,7 +17,8 @@ LAB = os.path.join(ROOT, "tools", "_ab", "lab")
 
 # [index, name] of the per-wave sums (tools/score_stats.py reads the same list)
 FIELDS = ["waves", "tiles", "cyc_loop", "cyc_stage", "cyc_epi_late", "cyc_compute", "cyc_epi_early", "cyc_wait",
-          "n_fast", "n_defer", "n_full", "cyc_full", "cyc_flush", "n_event_tiles", "cyc_detect", "cyc_defer"]
+          "n_fast", "n_defer", "n_full", "cyc_full", "cyc_flush", "n_event_tiles", "cyc_detect", "cyc_defer",
+          "cyc_dropmasked", "cyc_drain_ins", "cyc_insert_now", "n_unbounded", "n_rescan", "n_drain_steps"]
 
 
 def patch(src: str) -> str:
@@ -28,6 +29,24 @@ def patch(src: str) -> str:
 
     # device sums + host accessor
     rep("namespace lgx {\nnamespace {\n", "namespace lgx {\n__device__ unsigned long long g_lab[32];\nnamespace {\n")
+    # full-path split: the mask filter of the drain, the drain's insertions, the block's direct
+    # insertions; rescans summed over lanes; the drain's wave-serial insertion steps
+    rep("    float tau;       // filter threshold",
+        "    unsigned long long lab_dm = 0, lab_dr = 0, lab_in = 0, lab_unb = 0, lab_resc = 0, lab_steps = 0;\n"
+        "    float tau;       // filter threshold")
+    rep("            keys[mp] = key;\n            rescan();\n", "            keys[mp] = key;\n            ++lab_resc;\n            rescan();\n")
+    rep("        const uint32_t keep = drop_masked(a);\n",
+        "        const unsigned long long D0 = __builtin_amdgcn_s_memtime();\n"
+        "        const uint32_t keep = drop_masked(a);\n"
+        "        const unsigned long long D1 = __builtin_amdgcn_s_memtime();\n        lab_dm += D1 - D0;\n"
+        "        { int mx = pcnt; for (int m = 16; m > 0; m >>= 1) mx = max(mx, __shfl_xor(mx, m, 64)); lab_steps += 2 * mx; }\n")
+    rep("        pcnt = 0;\n        refresh_tau();\n    }\n",
+        "        pcnt = 0;\n        refresh_tau();\n        lab_dr += __builtin_amdgcn_s_memtime() - D1;\n    }\n")
+    rep("                                               uint32_t cmask) {\n",
+        "                                               uint32_t cmask) {\n        const unsigned long long I0 = __builtin_amdgcn_s_memtime();\n")
+    rep("            sync_from(ph);\n        }\n        refresh_tau();\n    }\n\n    template <bool MINMAX>",
+        "            sync_from(ph);\n        }\n        refresh_tau();\n        lab_in += __builtin_amdgcn_s_memtime() - I0;\n    }\n\n    template <bool MINMAX>")
+    rep("        } else {\n        }\n        drain(a);", "        } else {\n            ++lab_unb;\n        }\n        drain(a);")
     # per-wave accumulators at the loop
     rep("    const bool stage_after = STAGGER && !late;  // wave-uniform\n    for (int64_t t = 0; t < ntiles; ++t) {\n"
         "        const int64_t t0 = tile_start(t);\n"
@@ -88,11 +107,13 @@ def patch(src: str) -> str:
         "    const unsigned long long FL0 = __builtin_amdgcn_s_memtime();\n"
         "    st.flush(a, split, lane);\n"
         "    const unsigned long long L_flush = __builtin_amdgcn_s_memtime() - FL0;\n"
+        "    unsigned long long resc = st.lab_resc;\n"
+        "    for (int m = 32; m > 0; m >>= 1) resc += __shfl_xor(resc, m, 64);\n"
         "    if (lane == 0) {\n"
-        "        const unsigned long long v[16] = {1ull, L_tiles, L_loop, L_stage, L_epi_late, L_compute, L_epi_early,\n"
+        "        const unsigned long long v[22] = {1ull, L_tiles, L_loop, L_stage, L_epi_late, L_compute, L_epi_early,\n"
         "                                          L_wait, L_fast, L_defer, L_full, L_cyc_full, L_flush, L_ev, L_detect,\n"
-        "                                          L_defer_cyc};\n"
-        "        for (int j = 0; j < 16; ++j) atomicAdd(&g_lab[j], v[j]);\n"
+        "                                          L_defer_cyc, st.lab_dm, st.lab_dr, st.lab_in, st.lab_unb, resc, st.lab_steps};\n"
+        "        for (int j = 0; j < 22; ++j) atomicAdd(&g_lab[j], v[j]);\n"
         "    }\n"
         "}\n\ntemplate <int KSTEPS, bool MINMAX, int MODE = kTopK>")
     src += ("\nextern \"C\" int lgx_lab_stats(unsigned long long* out, int reset) {\n"

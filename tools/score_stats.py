@@ -55,6 +55,10 @@ def stats(fn, label):
     print("   per wave-tile: " + ", ".join(f"{k[2:]} {x:.3f}" for k, x in frac.items())
           + f"; cycles per full path {full_cyc:.0f}; flush {v['cyc_flush'] / max(1, v['waves']):.0f} per wave; "
             f"detect (incl. the MFMA results' wait) {det:.0f} per wave-tile; deferred path {dfr:.0f} per deferral", flush=True)
+    nf = max(1, v["n_full"])
+    print(f"   per full path: drop_masked {v['cyc_dropmasked'] / nf:.0f}, drain inserts {v['cyc_drain_ins'] / nf:.0f}, "
+          f"direct inserts {v['cyc_insert_now'] / nf:.0f} cycles (flush included); unbounded {v['n_unbounded'] / nf:.3f}; "
+          f"rescans per lane {v['n_rescan'] / nf / 64:.1f}, drain steps {v['n_drain_steps'] / nf:.1f}", flush=True)
 
 
 if ONLY in (None, "eval"):
