@@ -1586,58 +1586,88 @@ __global__ __launch_bounds__(kDenseWaves * 64) void strat_label_lds(const void* 
         return (uint32_t)l;
     };
     if (i_begin >= i_end) return;  // workgroup-uniform
+    auto mfmas = [&](int bf) {
+        const unsigned char* rowp = &img[bf][col * RB];
+        f32x16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+        for (int c = 0; c < KCH; ++c) {
+            const uint4 fr = *reinterpret_cast<const uint4*>(rowp + (((2 * c + h) ^ (col & 15)) * 16));
+            acc = F::mma(__builtin_bit_cast(typename F::chunk, fr), uf[c], acc);
+        }
+        return acc;
+    };
+    // labels, counts and the packed stores of the tile at e0
+    auto epilogue = [&](const f32x16& acc, int64_t e0) {
+        // whole tiles (all but a split's last) skip the per-item bounds tests
+        auto emit = [&](auto whole_tag) {
+            constexpr bool WHOLE = decltype(whole_tag)::value;
+            uint32_t* hu = hc + (wave * kUsersPerWave + col) * kHistStride;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t it = e0 + 8 * q + 4 * h;  // items it .. it + 3: acc rows 4q .. 4q + 3
+                const uint32_t l0 = label(acc[4 * q]), l1 = label(acc[4 * q + 1]);
+                const uint32_t l2 = label(acc[4 * q + 2]), l3 = label(acc[4 * q + 3]);
+                const uint32_t w = l0 | (l1 << 8) | (l2 << 16) | (l3 << 24);
+                if (hist) {  // items past the split's end are not counted
+                    if (WHOLE || it < i_end) atomicAdd(hu + l0, 1u);
+                    if (WHOLE || it + 1 < i_end) atomicAdd(hu + l1, 1u);
+                    if (WHOLE || it + 2 < i_end) atomicAdd(hu + l2, 1u);
+                    if (WHOLE || it + 3 < i_end) atomicAdd(hu + l3, 1u);
+                }
+                if (VEC4 && (WHOLE || it + 4 <= i_end)) {
+                    *reinterpret_cast<uint32_t*>(lab + it) = w;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (it + e < i_end) lab[it + e] = (int8_t)((w >> (8 * e)) & 255);
+                }
+            }
+        };
+        if (user_ok) {
+            if (e0 + 32 <= i_end) emit(std::true_type{});
+            else emit(std::false_type{});
+        }
+    };
+    // Staggered halves, as in score_dense_lds: the late waves (4-7) label tile t-1 right after the
+    // barrier and run tile t's MFMAs last, so each SIMD issues one wave's MFMAs while the other
+    // labels.  One loop per half (the halves take the same barriers), so only the late loop carries
+    // accumulators across its barrier.
+    const bool late = wave >= kDenseWaves / 2;  // wave-uniform
     load_tile(i_begin);
     store_tile(0);
     __syncthreads();
     int buf = 0;
-    for (int64_t i0 = i_begin; i0 < i_end; i0 += 32) {
-        const bool more = i0 + 32 < i_end;  // workgroup-uniform
-        if (more) load_tile(i0 + 32);
-        if (wave_on) {
-            const unsigned char* rowp = &img[buf][col * RB];
-            f32x16 acc;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-#pragma unroll
-            for (int c = 0; c < KCH; ++c) {
-                const uint4 fr = *reinterpret_cast<const uint4*>(rowp + (((2 * c + h) ^ (col & 15)) * 16));
-                acc = F::mma(__builtin_bit_cast(typename F::chunk, fr), uf[c], acc);
+    if (late) {
+        f32x16 acc;
+        int64_t prev_i0 = -1;
+        for (int64_t t0 = i_begin; t0 < i_end; t0 += 32) {
+            const bool more = t0 + 32 < i_end;  // workgroup-uniform
+            if (more) load_tile(t0 + 32);
+            if (wave_on) {
+                if (prev_i0 >= 0) epilogue(acc, prev_i0);
+                acc = mfmas(buf);
             }
-            // whole tiles (all but a split's last) skip the per-item bounds tests
-            auto emit = [&](auto whole_tag) {
-                constexpr bool WHOLE = decltype(whole_tag)::value;
-                uint32_t* hu = hc + (wave * kUsersPerWave + col) * kHistStride;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int64_t it = i0 + 8 * q + 4 * h;  // items it .. it + 3: acc rows 4q .. 4q + 3
-                    const uint32_t l0 = label(acc[4 * q]), l1 = label(acc[4 * q + 1]);
-                    const uint32_t l2 = label(acc[4 * q + 2]), l3 = label(acc[4 * q + 3]);
-                    const uint32_t w = l0 | (l1 << 8) | (l2 << 16) | (l3 << 24);
-                    if (hist) {  // items past the split's end are not counted
-                        if (WHOLE || it < i_end) atomicAdd(hu + l0, 1u);
-                        if (WHOLE || it + 1 < i_end) atomicAdd(hu + l1, 1u);
-                        if (WHOLE || it + 2 < i_end) atomicAdd(hu + l2, 1u);
-                        if (WHOLE || it + 3 < i_end) atomicAdd(hu + l3, 1u);
-                    }
-                    if (VEC4 && (WHOLE || it + 4 <= i_end)) {
-                        *reinterpret_cast<uint32_t*>(lab + it) = w;
-                    } else {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            if (it + e < i_end) lab[it + e] = (int8_t)((w >> (8 * e)) & 255);
-                    }
-                }
-            };
-            if (user_ok) {
-                if (i0 + 32 <= i_end) emit(std::true_type{});
-                else emit(std::false_type{});
-            }
+            if (more) store_tile(buf ^ 1);
+            prev_i0 = t0;
+            __syncthreads();
+            buf ^= 1;
         }
-        if (more) store_tile(buf ^ 1);
+        if (wave_on) epilogue(acc, prev_i0);
+        __syncthreads();  // the counts of the last tile, before the flush below
+    } else {
+        for (int64_t t0 = i_begin; t0 < i_end; t0 += 32) {
+            const bool more = t0 + 32 < i_end;  // workgroup-uniform
+            if (more) load_tile(t0 + 32);
+            if (wave_on) epilogue(mfmas(buf), t0);
+            if (more) store_tile(buf ^ 1);
+            __syncthreads();
+            buf ^= 1;
+        }
         __syncthreads();
-        buf ^= 1;
     }
-    if (hist) {  // the loop's last barrier has published every count
+    if (hist) {  // the last barrier has published every count
         const int64_t ub = ug * kDenseUsers;
         for (int e = threadIdx.x; e < kDenseUsers * kHistStride; e += kDenseWaves * 64) {
             const int uu = e / kHistStride, l = e % kHistStride;
