@@ -278,12 +278,18 @@ def dense_mask_offsets(mask: Tuple[torch.Tensor, torch.Tensor], n_items: int, c0
     return rid * n_items + sx.to(torch.int64)
 
 
-def dense_chunk_users(n_items: int, chunk_bytes: int = 256 << 20) -> int:
+# the dense route's f32 score chunk: 1 GiB ranks the long-mask users of the evaluation shapes in one
+# chunk (Amazon-book: 737 users, 0.63 -> 0.44 ms against 256 MiB; tools/chunk_probe.py,
+# profiles/r05_chunk_probe.txt)
+DENSE_CHUNK_BYTES = 1 << 30
+
+
+def dense_chunk_users(n_items: int, chunk_bytes: int = DENSE_CHUNK_BYTES) -> int:
     return max(1, chunk_bytes // max(1, 4 * n_items))
 
 
 def score_topk_dense_masked(Q: torch.Tensor, items: torch.Tensor, k: int, user_rows: torch.Tensor,
-                            mask: Tuple[torch.Tensor, torch.Tensor], chunk_bytes: int = 256 << 20,
+                            mask: Tuple[torch.Tensor, torch.Tensor], chunk_bytes: int = DENSE_CHUNK_BYTES,
                             offsets: Optional[Sequence[torch.Tensor]] = None) -> torch.Tensor:
     """The ranking score_topk returns (idx int32 [B, k]; raw scores ranked, ties to the lower item id)
     by another route, for users whose mask is long: their dense raw score rows (lgx_score_dense), the
