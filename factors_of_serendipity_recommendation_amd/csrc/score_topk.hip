@@ -289,27 +289,34 @@ struct WaveTopKT {
         return a.susp + (((size_t)b * a.n_splits + sp) * 2 + h) * kSuspSlots;
     }
 
-    // new worst entry: 8 keys (four 16-byte reads issued together) per LDS round trip
+    // new worst entry: 8 keys (four 16-byte reads issued together) per LDS round trip.  The whole
+    // 8-key groups need no bounds test; the tail group (k % 8 keys) reads only the pairs it needs
+    // when it holds at most 4 (k = 20: two whole groups and two reads)
+    template <int N, bool MASK>
+    __device__ __forceinline__ void rescan_group(int j0, uint64_t& m, int& p) const {
+        uint64_t v[N];
+#pragma unroll
+        for (int j = 0; j < N; j += 2) {
+            const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(keys + j0 + j);
+            v[j] = q.x;
+            v[j + 1] = q.y;
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const uint64_t x = (!MASK || j0 + j < k) ? v[j] : ~0ull;
+            if (x < m) {
+                m = x;
+                p = j0 + j;
+            }
+        }
+    }
     __device__ __forceinline__ void rescan() {
         uint64_t m = ~0ull;
         int p = 0;
-        for (int j0 = 0; j0 < k; j0 += 8) {
-            uint64_t v[8];
-#pragma unroll
-            for (int j = 0; j < 8; j += 2) {
-                const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(keys + j0 + j);
-                v[j] = q.x;
-                v[j + 1] = q.y;
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const uint64_t x = (j0 + j < k) ? v[j] : ~0ull;
-                if (x < m) {
-                    m = x;
-                    p = j0 + j;
-                }
-            }
-        }
+        const int kw = k & ~7;  // keys in whole groups
+        for (int j0 = 0; j0 < kw; j0 += 8) rescan_group<8, false>(j0, m, p);
+        if (k - kw > 4) rescan_group<8, true>(kw, m, p);
+        else if (k > kw) rescan_group<4, true>(kw, m, p);
         mp = p;
         kmin = m;
     }
