@@ -294,51 +294,83 @@ __global__ __launch_bounds__(kFoldUsers) void foldout_staged_kernel(const int32_
 // np.mean(a, axis=0) of a C-contiguous float32 [rows, cols] array, as numpy computes it: per column a
 // float32 sum over the rows in row order (numpy's axis-0 add.reduce adds whole rows, no pairwise
 // blocking), then one float32 division by the row count.  The order makes each column one chain of
-// dependent adds; what must not sit on that chain is the load latency.  A workgroup owns 64 columns:
-// its 512 threads stage blocks of kMeanRows rows into LDS (coalesced 256-B row pieces, the next block
-// in flight while the current one is summed) and wave 0 adds them lane = column, row by row.
+// dependent adds; what must not sit on that chain is the load latency.  A workgroup owns
+// kMeanCols = 16 columns, so that a [rows, 100] array (batch_test's 5 x 20 curves) spreads its loads
+// over 7 CUs: with 64 columns per workgroup two CUs each pulled ~25 GB/s and the kernel took 10 ns
+// per row (0.55 ms at 52 643 rows).  Its 512 threads stage blocks of kMeanRows rows into LDS (one
+// block ahead in registers while the current one is summed), and lanes 0-15 of wave 0 add them,
+// lane = column, row by row, 64 rows per LDS round trip with the next 64 in flight (the image is
+// column-major, each column's rows 16-B aligned and 4 banks from the next column's).
 constexpr int kMeanRows = 256;
 constexpr int kMeanWaves = 8;
+constexpr int kMeanCols = 16;
+constexpr int kMeanPad = kMeanRows + 4;
 __global__ __launch_bounds__(kMeanWaves * 64) void column_mean_kernel(const float* __restrict__ src, int64_t rows,
                                                                      int64_t cols, float* __restrict__ out) {
-    __shared__ float blk[2][kMeanRows][64];
+    __shared__ __attribute__((aligned(16))) float blk[2][kMeanCols][kMeanPad];
+    constexpr int kRowsPerPass = kMeanWaves * 64 / kMeanCols;  // 32 rows per load instruction of the workgroup
+    constexpr int J = kMeanRows / kRowsPerPass;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int64_t c0 = (int64_t)blockIdx.x * 64;
-    const int64_t col = c0 + lane;
-    float nx[kMeanRows / kMeanWaves];
-    auto load = [&](int64_t r0) {
+    const int cl = t % kMeanCols, rr = t / kMeanCols;  // staging: column cl of rows rr + 32 j
+    const int64_t c0 = (int64_t)blockIdx.x * kMeanCols;
+    const int64_t lcol = c0 + cl;
+    float nxa[J], nxb[J];
+    auto load = [&](float (&nx)[J], int64_t r0) {
 #pragma unroll
-        for (int j = 0; j < kMeanRows / kMeanWaves; ++j) {
-            const int64_t r = r0 + kMeanWaves * j + w;
-            nx[j] = (r < rows && col < cols) ? src[r * cols + col] : 0.0f;
+        for (int j = 0; j < J; ++j) {
+            const int64_t r = r0 + kRowsPerPass * j + rr;
+            nx[j] = (r < rows && lcol < cols) ? src[r * cols + lcol] : 0.0f;
         }
     };
-    auto store = [&](int b) {
+    auto store = [&](const float (&nx)[J], int b) {
 #pragma unroll
-        for (int j = 0; j < kMeanRows / kMeanWaves; ++j) blk[b][kMeanWaves * j + w][lane] = nx[j];
+        for (int j = 0; j < J; ++j) blk[b][cl][kRowsPerPass * j + rr] = nx[j];
     };
     float acc = -0.0f;  // -0 + x == x for every x: the same sums as numpy's, which starts from row 0
-    load(0);
-    store(0);
-    __syncthreads();
-    int b = 0;
-    for (int64_t r0 = 0; r0 < rows; r0 += kMeanRows) {
-        const bool more = r0 + kMeanRows < rows;
-        if (more) load(r0 + kMeanRows);
-        if (w == 0) {
-            const int n = (int)min((int64_t)kMeanRows, rows - r0);
-            if (n == kMeanRows) {
-#pragma unroll 16
-                for (int r = 0; r < kMeanRows; ++r) acc = acc + blk[b][r][lane];  // row order
-            } else {
-                for (int r = 0; r < n; ++r) acc = acc + blk[b][r][lane];
+    auto sum = [&](int b, int64_t r0) {
+        if (w != 0) return;
+        const int n = (int)min((int64_t)kMeanRows, rows - r0);
+        const float* cp = &blk[b][lane % kMeanCols][0];
+        if (n == kMeanRows) {
+            float4 v[2][16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[0][q] = *reinterpret_cast<const float4*>(cp + 4 * q);
+#pragma unroll
+            for (int r = 0; r < kMeanRows; r += 64) {
+                const int cur = (r / 64) & 1;
+                if (r + 64 < kMeanRows) {
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) v[cur ^ 1][q] = *reinterpret_cast<const float4*>(cp + r + 64 + 4 * q);
+                }
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {  // row order
+                    acc = acc + v[cur][q].x;
+                    acc = acc + v[cur][q].y;
+                    acc = acc + v[cur][q].z;
+                    acc = acc + v[cur][q].w;
+                }
             }
+        } else {
+            for (int r = 0; r < n; ++r) acc = acc + cp[r];
         }
-        if (more) store(b ^ 1);
+    };
+    // block r0 is in LDS buffer b, block r0 + R in registers `next`; block r0 + 2R goes into `into`
+    auto step = [&](int64_t r0, int b, const float (&next)[J], float (&into)[J]) {
+        if (r0 + 2 * kMeanRows < rows) load(into, r0 + 2 * kMeanRows);
+        sum(b, r0);
+        if (r0 + kMeanRows < rows) store(next, b ^ 1);  // buffer b ^ 1 was last read before the previous barrier
         __syncthreads();
-        b ^= 1;
+    };
+    load(nxa, 0);
+    store(nxa, 0);
+    if (kMeanRows < rows) load(nxb, kMeanRows);
+    __syncthreads();
+    for (int64_t r0 = 0; r0 < rows; r0 += 2 * kMeanRows) {
+        step(r0, 0, nxb, nxa);
+        if (r0 + kMeanRows < rows) step(r0 + kMeanRows, 1, nxa, nxb);
     }
-    if (w == 0 && col < cols) out[col] = rows > 0 ? acc / (float)rows : NAN;
+    const int64_t col = c0 + lane;
+    if (w == 0 && lane < kMeanCols && col < cols) out[col] = rows > 0 ? acc / (float)rows : NAN;
 }
 
 template <int R>
@@ -399,7 +431,7 @@ extern "C" int lgx_column_mean_f32(const float* src, int64_t rows, int64_t cols,
     LGX_REQUIRE(rows < (1LL << 24), LGX_ERR_UNSUPPORTED,
                 "lgx_column_mean_f32: %lld rows (the float32 row count is exact below 2^24)", (long long)rows);
     if (cols == 0) return LGX_OK;
-    column_mean_kernel<<<(unsigned)ceil_div(cols, (int64_t)64), kMeanWaves * 64, 0, as_hip(stream)>>>(src, rows, cols, out);
+    column_mean_kernel<<<(unsigned)ceil_div(cols, (int64_t)kMeanCols), kMeanWaves * 64, 0, as_hip(stream)>>>(src, rows, cols, out);
     LGX_LAUNCH_CHECK();
     return LGX_OK;
 }
