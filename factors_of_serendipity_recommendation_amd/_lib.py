@@ -108,6 +108,8 @@ SIGNATURES = {
     "lgx_topk_rows": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _c_int, _vp, _vp, _vp]),
     "lgx_foldout_metrics": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "lgx_column_mean_f32": (_c_int, [_vp, _c_i64, _c_i64, _vp, _vp]),
+    "lgx_test_metrics_workspace": (_c_int, [_c_i64, _c_int, _sz_p]),
+    "lgx_test_metrics": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "lgx_gather_scores": (_c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp]),
     "lgx_synth_edges": (_c_int, [ctypes.c_uint64, _vp, _c_i64, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp]),
     "lgx_fill_normal": (_c_int, [_vp, _c_i64, ctypes.c_float, ctypes.c_uint64, _c_int, _vp]),

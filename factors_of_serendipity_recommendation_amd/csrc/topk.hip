@@ -373,6 +373,78 @@ __global__ __launch_bounds__(kMeanWaves * 64) void column_mean_kernel(const floa
     if (w == 0 && lane < kMeanCols && col < cols) out[col] = rows > 0 ? acc / (float)rows : NAN;
 }
 
+// Procedure.Test's metrics (Procedure.py:60-72 -> utils.getLabel, RecallPrecision_ATk, NDCGatK_r,
+// code/utils.py:218-285) for every test user at once: one thread per user marks which of its top-k
+// items are test items (binary search in its sorted, deduplicated test list; the list's own length,
+// duplicates included, is test_len), forms the per-user terms of each
+// topk in float64 -- right / |test|, right, dcg / idcg with idcg over min(k, |test|) ranks and the
+// reference's idcg == 0 -> 1, NaN -> 0 -- and the workgroup adds them in a fixed order; a second
+// launch adds the workgroups' partial sums in workgroup order.  Deterministic; the reference adds
+// the same terms batch by batch, so the sums agree to float64 rounding.
+constexpr int kTmUsers = 256;
+constexpr int kTmMaxTopks = 8;
+__global__ __launch_bounds__(kTmUsers) void test_metrics_kernel(const int32_t* __restrict__ rankings, int64_t users,
+                                                                int k, const int64_t* __restrict__ truth_indptr,
+                                                                const int32_t* __restrict__ truth_indices,
+                                                                const int64_t* __restrict__ test_len,
+                                                                const int32_t* __restrict__ topks, int n_topks,
+                                                                const double* __restrict__ inv_log2,
+                                                                double* __restrict__ partial) {
+    __shared__ double red[kTmUsers];
+    const int t = threadIdx.x;
+    const int64_t u = blockIdx.x * (int64_t)kTmUsers + t;
+    double term[3 * kTmMaxTopks];
+#pragma unroll
+    for (int i = 0; i < 3 * kTmMaxTopks; ++i) term[i] = 0.0;
+    if (u < users) {
+        const int64_t a = truth_indptr[u], L = truth_indptr[u + 1] - a;
+        const int64_t n_test = test_len ? test_len[u] : L;  // len(test list), duplicates included
+        const int32_t* tl = truth_indices + a;
+        const int32_t* rk = rankings + u * k;
+        int right = 0, tp = 0;
+        double dcg = 0.0, idcg = 0.0;
+        for (int j = 0; j < k; ++j) {
+            const int32_t x = rk[j];
+            int64_t lo = 0, hi = L;  // first position with tl[pos] >= x
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (tl[mid] < x) lo = mid + 1;
+                else hi = mid;
+            }
+            const bool hit = x >= 0 && lo < L && tl[lo] == x;
+            right += hit ? 1 : 0;
+            dcg += hit ? inv_log2[j] : 0.0;  // r * (1 / log2(j + 2)), summed over j in rank order
+            if (j < n_test) idcg += inv_log2[j];
+            while (tp < n_topks && topks[tp] == j + 1) {
+                const double id = idcg == 0.0 ? 1.0 : idcg;
+                const double nd = dcg / id;
+                term[3 * tp + 0] = (double)right / (double)n_test;  // recall: right / len(test) (NaN as numpy at 0)
+                term[3 * tp + 1] = (double)right;               // precision: summed, then / k on the host
+                term[3 * tp + 2] = nd != nd ? 0.0 : nd;
+                ++tp;
+            }
+        }
+    }
+    for (int i = 0; i < 3 * n_topks; ++i) {
+        red[t] = term[i];
+        __syncthreads();
+        for (int s = kTmUsers / 2; s > 0; s >>= 1) {
+            if (t < s) red[t] += red[t + s];
+            __syncthreads();
+        }
+        if (t == 0) partial[blockIdx.x * (int64_t)(3 * n_topks) + i] = red[0];
+        __syncthreads();
+    }
+}
+
+__global__ void test_metrics_sum_kernel(const double* __restrict__ partial, int64_t blocks, int n, double* __restrict__ out) {
+    const int i = threadIdx.x;
+    if (i >= n) return;
+    double acc = 0.0;
+    for (int64_t b = 0; b < blocks; ++b) acc += partial[b * n + i];
+    out[i] = acc;
+}
+
 template <int R>
 int launch_topk_rows(const float* S, int64_t rows, int64_t cols, int64_t ld, int k, int32_t* out_idx,
                      float* out_val, bool vec, hipStream_t st) {
@@ -432,6 +504,34 @@ extern "C" int lgx_column_mean_f32(const float* src, int64_t rows, int64_t cols,
                 "lgx_column_mean_f32: %lld rows (the float32 row count is exact below 2^24)", (long long)rows);
     if (cols == 0) return LGX_OK;
     column_mean_kernel<<<(unsigned)ceil_div(cols, (int64_t)kMeanCols), kMeanWaves * 64, 0, as_hip(stream)>>>(src, rows, cols, out);
+    LGX_LAUNCH_CHECK();
+    return LGX_OK;
+}
+
+extern "C" int lgx_test_metrics_workspace(int64_t users, int n_topks, size_t* bytes) {
+    LGX_REQUIRE(users >= 0 && n_topks >= 1 && n_topks <= kTmMaxTopks && bytes, LGX_ERR_INVALID_ARG,
+                "lgx_test_metrics_workspace: bad arguments");
+    *bytes = (size_t)std::max<int64_t>(1, ceil_div(users, (int64_t)kTmUsers)) * 3 * n_topks * sizeof(double);
+    return LGX_OK;
+}
+
+extern "C" int lgx_test_metrics(const int32_t* rankings, int64_t users, int k, const int64_t* truth_indptr,
+                                const int32_t* truth_indices, const int64_t* test_len, const int32_t* topks, int n_topks,
+                                const double* inv_log2, double* sums, void* ws, size_t ws_bytes,
+                                lgx_stream_t stream) {
+    LGX_REQUIRE(users >= 0 && k >= 1 && n_topks >= 1 && n_topks <= kTmMaxTopks, LGX_ERR_INVALID_ARG,
+                "lgx_test_metrics: bad sizes (1 <= n_topks <= %d)", kTmMaxTopks);
+    LGX_REQUIRE(sums && topks && inv_log2 && (users == 0 || (rankings && truth_indptr)), LGX_ERR_INVALID_ARG,
+                "lgx_test_metrics: null pointer");
+    size_t need = 0;
+    lgx_test_metrics_workspace(users, n_topks, &need);
+    LGX_REQUIRE(ws && ws_bytes >= need, LGX_ERR_WORKSPACE, "lgx_test_metrics: workspace %zu < %zu bytes", ws_bytes, need);
+    const int64_t blocks = std::max<int64_t>(1, ceil_div(users, (int64_t)kTmUsers));
+    double* partial = static_cast<double*>(ws);
+    test_metrics_kernel<<<(unsigned)blocks, kTmUsers, 0, as_hip(stream)>>>(rankings, users, k, truth_indptr, truth_indices,
+                                                                         test_len, topks, n_topks, inv_log2, partial);
+    LGX_LAUNCH_CHECK();
+    test_metrics_sum_kernel<<<1, 64, 0, as_hip(stream)>>>(partial, blocks, 3 * n_topks, sums);
     LGX_LAUNCH_CHECK();
     return LGX_OK;
 }

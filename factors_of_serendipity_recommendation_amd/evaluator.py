@@ -209,6 +209,9 @@ class _TestLists:
         self.M = int(max(n_items, int(flat.max()) + 1 if flat.size else 0, 1))
         keys = np.repeat(np.arange(n, dtype=np.int64), self.recall_n) * self.M + flat
         self.keys = torch.unique(torch.from_numpy(keys).to(dev))  # sorted
+        # the same lists as a CSR (sorted, deduplicated) for lgx_test_metrics
+        bounds = torch.arange(n + 1, device=dev, dtype=torch.int64) * self.M
+        self.truth = (torch.searchsorted(self.keys, bounds), (self.keys % self.M).to(torch.int32))
 
     def route(self, n_items: int, k: int, d: int) -> _Route:
         key = (n_items, k, d)
@@ -248,8 +251,8 @@ class _TestLists:
 
 def Test(dataset, Recmodel, epoch=0, w=None, multicore=0, topks: Sequence[int] = (20,)) -> Dict:
     """Procedure.Test on the fused engine: one propagation, one fused score+mask+top-k launch for
-    all test users (sigmoid scores, positives set to -(1<<10) as Procedure.py:134), the hit matrix
-    and the float64 metric sums on the device."""
+    all test users (sigmoid scores, positives set to -(1<<10) as Procedure.py:134), and one launch
+    for the hits and the float64 metric sums (lgx_test_metrics)."""
     Recmodel = Recmodel.eval()
     max_K = max(topks)
     results = {"precision": np.zeros(len(topks)), "recall": np.zeros(len(topks)), "ndcg": np.zeros(len(topks))}
@@ -258,7 +261,9 @@ def Test(dataset, Recmodel, epoch=0, w=None, multicore=0, topks: Sequence[int] =
         tl = _TestLists.get(dataset, all_items.shape[0], all_users.device)
         idx = tl.route(all_items.shape[0], max_K, all_items.shape[1]).topk(all_users, all_items, max_K,
                                                                           -float(1 << 10), True)
-        res = _metrics_dev(tl.hit_mask(idx), tl.recall_n_dev, topks)
+        # getLabel + RecallPrecision_ATk + NDCGatK_r for every user in one launch (lgx_test_metrics)
+        sums = ops.test_metrics(idx, tl.truth, topks, tl.recall_n_dev).cpu().numpy()
+        res = {"recall": sums[0], "precision": sums[1] / np.asarray(topks, dtype=np.float64), "ndcg": sums[2]}
         for key in results:
             results[key] = res[key] / float(len(tl.users))
     return results

@@ -349,9 +349,24 @@ def topk_rows(S: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
     return idx, val
 
 
+_SMALL_CONST: dict = {}
+
+
+def _device_const(key: tuple, make) -> torch.Tensor:
+    """A small read-only device tensor built once per key (a host-to-device copy per evaluation call
+    cost as much as the metric kernel itself)."""
+    t = _SMALL_CONST.get(key)
+    if t is None:
+        t = _SMALL_CONST[key] = make()
+    return t
+
+
 def inv_log2_table(k: int, device) -> torch.Tensor:
-    """1.0/log2(i+2) with the host libm (as the C++ evaluator computes it, evaluate_foldout.h:80,84)."""
-    return torch.tensor([1.0 / math.log2(i + 2) for i in range(k)], dtype=torch.float64, device=device)
+    """1.0/log2(i+2) with the host libm (as the C++ evaluator computes it, evaluate_foldout.h:80,84);
+    cached per (k, device), read-only."""
+    return _device_const(("inv_log2", k, str(torch.device(device))),
+                         lambda: torch.tensor([1.0 / math.log2(i + 2) for i in range(k)], dtype=torch.float64,
+                                              device=device))
 
 
 def foldout_metrics(rankings: torch.Tensor, truth: Tuple[torch.Tensor, torch.Tensor]) -> torch.Tensor:
@@ -378,6 +393,38 @@ def column_mean(x: torch.Tensor) -> torch.Tensor:
     _lib.check(_lib.lib().lgx_column_mean_f32(x.data_ptr(), x.shape[0], x.shape[1], out.data_ptr(),
                                               _stream_ptr(x.device)), "lgx_column_mean_f32")
     return out
+
+
+def test_metrics(rankings: torch.Tensor, truth: Tuple[torch.Tensor, torch.Tensor], topks: Sequence[int],
+                 test_len: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Procedure.Test's metric sums over all users (Procedure.py:60-72, ``lgx_test_metrics``): rankings
+    int32 [users, max(topks)], truth = sorted deduplicated test lists as a CSR, test_len = the lists'
+    lengths with duplicates (int64 [users]) -> f64 [3, len(topks)] on the device: per topk the sums of
+    recall, of right (precision * topk) and of ndcg, in the order of ``topks``."""
+    require_gpu(rankings)
+    r = rankings.to(torch.int32).contiguous()
+    users, k = r.shape
+    ks = [int(x) for x in topks]
+    if not ks or len(ks) > 8 or min(ks) < 1 or max(ks) != k:
+        raise ValueError(f"test_metrics: topks {ks} with rankings of width {k} (1..8 topks, max = width)")
+    order = sorted(range(len(ks)), key=lambda i: ks[i])
+    tk = _device_const(("topks", tuple(ks[i] for i in order), str(r.device)),
+                       lambda: torch.tensor([ks[i] for i in order], dtype=torch.int32, device=r.device))
+    tl = inv_log2_table(k, r.device)
+    L = _lib.lib()
+    ws = ctypes.c_size_t(0)
+    _lib.check(L.lgx_test_metrics_workspace(users, len(ks), ctypes.byref(ws)), "lgx_test_metrics_workspace")
+    work = torch.empty(max(ws.value, 8), dtype=torch.uint8, device=r.device)
+    out = torch.empty((len(ks), 3), dtype=torch.float64, device=r.device)
+    tlen = test_len.to(torch.int64).contiguous() if test_len is not None else None
+    _lib.check(L.lgx_test_metrics(r.data_ptr(), users, k, truth[0].data_ptr(), truth[1].data_ptr(), _ptr(tlen),
+                                  tk.data_ptr(), len(ks), tl.data_ptr(), out.data_ptr(), work.data_ptr(), ws.value,
+                                  _stream_ptr(r.device)), "lgx_test_metrics")
+    if order == list(range(len(ks))):
+        return out.t()
+    inv = _device_const(("topks_inv", tuple(order), str(r.device)),
+                        lambda: torch.tensor(order, device=r.device).argsort())
+    return out[inv].t()
 
 
 def gather_scores(emb_user: torch.Tensor, emb_item: torch.Tensor, cand: Tuple[torch.Tensor, torch.Tensor],

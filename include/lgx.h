@@ -25,6 +25,7 @@
  *   lgx_score_minmax       np.max / np.min of the U x I dot     recommend.py:163-164, 377; utils.py:500-529
  *   lgx_topk_rows          c_top_k_array_index                  LightGCN-tf/evaluator/cpp/include/tools.h:13-33
  *   lgx_foldout_metrics    evaluate_foldout                     LightGCN-tf/evaluator/cpp/include/evaluate_foldout.h:115-195
+ *   lgx_test_metrics       Procedure.Test metric sums           lightGCN/LightGCN-PyTorch-master/code/Procedure.py:60-72
  *   lgx_gather_scores      accuracy_cf / elasticity_item per-user candidate dot  recommend.py:167-171, 214-217
  *   lgx_parse_lines_*      Loader / Data file parsing            code/dataloader.py:247-277; load_data.py:27-48
  *   lgx_strat_labels/select create_candidates_stratification   recommend.py:314-452
@@ -275,6 +276,22 @@ int lgx_foldout_metrics(const int32_t* rankings, int64_t users, int k, const int
  * rows = 0 gives NaN as np.mean of an empty axis does.
  */
 int lgx_column_mean_f32(const float* src, int64_t rows, int64_t cols, float* out, lgx_stream_t stream);
+/*
+ * Procedure.Test's metric sums (lightGCN/LightGCN-PyTorch-master/code/Procedure.py:60-72 over
+ * code/utils.py:218-285: getLabel, RecallPrecision_ATk, NDCGatK_r) for all test users at once:
+ * rankings [users, k] int32 (k = max topks), test lists as a CSR with each list sorted ascending
+ * (truth_indptr [users+1] int64, truth_indices int32, sorted and deduplicated), test_len [users] int64
+ * = len(test list) with duplicates (nullable: the CSR lengths), topks [n_topks] int32 ascending in [1, k]
+ * (n_topks <= 8), inv_log2 [k] f64 = 1/log2(j+2) -> sums [3, n_topks] f64 = per topk the sums over
+ * users of right/|test| (recall), right (precision: divide by the topk) and dcg/idcg (ndcg, idcg over
+ * min(topk, |test|) ranks, idcg == 0 -> 1, NaN -> 0).  Summed in a fixed order; workspace from
+ * lgx_test_metrics_workspace.
+ */
+int lgx_test_metrics_workspace(int64_t users, int n_topks, size_t* bytes);
+int lgx_test_metrics(const int32_t* rankings, int64_t users, int k, const int64_t* truth_indptr,
+                     const int32_t* truth_indices, const int64_t* test_len, const int32_t* topks, int n_topks,
+                     const double* inv_log2,
+                     double* sums, void* ws, size_t ws_bytes, lgx_stream_t stream);
 
 /* ---------------------------------------------------------------- a11/a12: candidate similarity */
 /*

@@ -225,3 +225,39 @@ def test_evaluator_route_splits_long_masks():
     assert torch.isfinite(got[heavy]).all()
     assert (got[heavy] >= (kth - 1e-5 * kth.abs().clamp(min=1.0))[heavy]).all()
     assert torch.equal(idx[~heavy], ref[~heavy])  # the light users are the fused launch's own result
+
+
+@pytest.mark.parametrize("topks", [[20], [1, 5, 20], [20, 5], [100, 10, 50]])
+def test_test_metrics_kernel_matches_host_restatement(topks):
+    """lgx_test_metrics (Procedure.Test's getLabel + RecallPrecision_ATk + NDCGatK_r sums in one launch)
+    against the host restatement of utils.py:218-285 on the same rankings: short and power-law test
+    lists (binary search over thousands of items), duplicated test items (len() counts them, a hit
+    does not), rankings padded with -1, several topks in any order.  float64 sums in another order:
+    1e-12 relative."""
+    rng = np.random.default_rng(len(topks) * 7 + max(topks))
+    n_users, n_items, K = 3000, 20000, max(topks)
+    lens = np.minimum(rng.zipf(1.6, n_users), 5000)
+    truths = [list(rng.choice(n_items, size=int(L), replace=False)) for L in lens]
+    for u in range(0, n_users, 37):  # duplicates
+        if truths[u]:
+            truths[u] = truths[u] + truths[u][:2]
+    rank = np.stack([rng.choice(n_items, size=K, replace=False) for _ in range(n_users)]).astype(np.int32)
+    for u in range(n_users):  # plant hits at random ranks
+        t = truths[u]
+        for j in rng.choice(K, size=min(len(t), int(rng.integers(0, 6))), replace=False):
+            rank[u, j] = t[int(rng.integers(0, len(t)))]
+    rank[::53, -3:] = -1
+    # a ranking must not repeat an item (getLabel counts each position): drop planted repeats
+    for u in range(n_users):
+        _, first = np.unique(rank[u], return_index=True)
+        dup = np.setdiff1d(np.arange(K), first)
+        rank[u, dup] = -1
+    recall_n = np.array([len(t) for t in truths], dtype=np.int64)
+    hit = np.array([[x in set(t) for x in rank[u]] for u, t in enumerate(truths)], dtype=float)
+    want = evaluator._metrics(hit, recall_n, topks)
+    truth = ops.lists_to_device_csr([sorted(set(t)) for t in truths], DEV, sort=True)
+    got = ops.test_metrics(torch.from_numpy(rank).to(DEV), truth, topks,
+                           torch.from_numpy(recall_n).to(DEV)).cpu().numpy()
+    np.testing.assert_allclose(got[0], want["recall"], rtol=1e-12)
+    np.testing.assert_allclose(got[1] / np.asarray(topks, dtype=float), want["precision"], rtol=1e-12)
+    np.testing.assert_allclose(got[2], want["ndcg"], rtol=1e-12)

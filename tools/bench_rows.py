@@ -493,7 +493,7 @@ def row_eval(rows, reps, tmpdir, cfg_name):
         t2 = sync_t()
         idx = tl.route(all_items.shape[0], 20, cfg.d).topk(all_users, all_items, 20, -float(1 << 10), True)
         t3 = sync_t()
-        evaluator._metrics_dev(tl.hit_mask(idx), tl.recall_n_dev, [20])
+        ops.test_metrics(idx, tl.truth, [20], tl.recall_n_dev).cpu()  # as evaluator.Test: one launch + the sums' copy
         t4 = sync_t()
         for k_, a_, b_ in (("propagation", t0, t1), ("lists", t1, t2), ("score_topk", t2, t3),
                            ("hits_metrics", t3, t4)):
