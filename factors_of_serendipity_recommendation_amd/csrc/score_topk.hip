@@ -148,7 +148,12 @@ constexpr int kPendBf16Lds = 12;
 // for them; fp32 at d = 256 keeps 4 (two 64 KB tiles and four waves' lists fill the 160 KB).  fp32
 // with 12 (profiles/r04_eval_probe_ab.txt, masked top-20): Gowalla shape 3.67 -> 3.30 ms, Amazon-book
 // shape 17.6 -> 16.6 ms
-__host__ __device__ constexpr int lds_pend(bool f32, int ksteps) { return f32 && ksteps > 8 ? kPendSlots : kPendBf16Lds; }
+// ... and 16 in the 4-wave fp32 walk up to d = 128 (one wave per SIMD, LDS to spare: 4 x 14 KB of
+// lists beside a 4-tile ring at d = 64), where an exact path is the wave's own time and fewer of
+// them pay (Gowalla shape, profiles/r05_pend16_ab.txt: route 3.12 -> 3.05 ms)
+__host__ __device__ constexpr int lds_pend(bool f32, int ksteps, int waves = 8) {
+    return f32 && ksteps > 8 ? kPendSlots : f32 && waves == 4 ? 16 : kPendBf16Lds;
+}
 __host__ __device__ constexpr size_t list_keys_per_wave(int k) { return (size_t)kUsersPerWave * kstride(k) + kListSpare; }
 // ... then one int per lane: the count of its parked keys (kSuspSlots)
 __host__ __device__ constexpr size_t list_bytes_per_wave(int k, int pend = kPendSlots) {
@@ -809,7 +814,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5, col = lane & 31;
-    typedef WaveTopKT<lds_pend(F32, KSTEPS)> TopK;
+    typedef WaveTopKT<lds_pend(F32, KSTEPS, WAVES)> TopK;
     uint64_t* lk = reinterpret_cast<uint64_t*>(smem + (size_t)nbuf * G::TILE + (size_t)wave * list_bytes_per_wave(k, TopK::kPend));
 
     // workgroup -> (catalog split, user tile)
@@ -1719,7 +1724,7 @@ bool lds_eligible(int dtype, int64_t d, int k) {
         return d % 32 == 0 && d >= 32 && d <= 256 && k <= 32 &&
                2 * (size_t)kTileItems * d * 2 + 8 * list_bytes_per_wave(k, kPendBf16Lds) <= kLdsBytes;
     if (dtype != LGX_DTYPE_F32 || d % 64 != 0 || d < 64 || d > 256 || k > 32) return false;
-    return 2 * (size_t)kTileItems * d * 4 + (size_t)kF32LdsWaves * list_bytes_per_wave(k, lds_pend(true, (int)(d / 16))) <=
+    return 2 * (size_t)kTileItems * d * 4 + (size_t)kF32LdsWaves * list_bytes_per_wave(k, lds_pend(true, (int)(d / 16), kF32LdsWaves)) <=
            kLdsBytes;
 }
 
@@ -1841,7 +1846,7 @@ int launch_bf16_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t s
 template <int KS, bool MM, int MODE, int WAVES = kF32LdsWaves>
 int launch_f32_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
     typedef LdsGeom<KS, WAVES, 2, 4> G;
-    const size_t lists = (size_t)WAVES * list_bytes_per_wave(a.k, lds_pend(true, KS));
+    const size_t lists = (size_t)WAVES * list_bytes_per_wave(a.k, lds_pend(true, KS, WAVES));
     const int nbuf = lds_ring_buffers(G::TILE, lists, 1);
     const size_t shmem = (size_t)nbuf * G::TILE + lists;
     if (shmem > kLdsBytes) {
