@@ -133,14 +133,21 @@ def clear_caches() -> None:
 # items that reaches the running threshold takes an exact search.  On propagated LightGCN tables a
 # user's train items are among its best scores, and power-law users mask thousands of them
 # (tools/mask_probe.py, profiles/r05_mask_probe.txt: the ~5 % of Gowalla-shape users above 64 masked
-# items cost 1.6 ms of the 5.1 ms fused launch).  A dense row costs about n_items * d, so the
-# threshold grows with it (tools/route_probe.py, profiles/r05_route_probe.txt: best near 64 at the
-# Gowalla shape, 256-1024 at the Amazon-book shape).
+# items cost 1.6 ms of the 5.1 ms fused launch).  The dense route runs beside the fused launch
+# (_Route.topk): while the fused walk leaves CUs idle -- fewer users than one round of its
+# workgroups, 256 x 256 users at d <= 128 (8 waves x 32 users), 256 x 128 above -- dense rows cost
+# nothing until they outlast it, and the threshold is the floor of 64 (profiles/r05_route_probe_side.txt:
+# Amazon-book shape 14.70 ms at 357, 14.14 ms at 64; Gowalla flat from 64 to 128).  Otherwise a
+# dense row adds its n_items * d to the call and the threshold grows with it (best near 64 at the
+# Gowalla shape, 256-1024 at the Amazon-book shape when the two parts ran one after the other,
+# profiles/r05_route_probe.txt).
 DENSE_MASK_MIN = 64
 DENSE_MAX_ITEMS = 1 << 18
 
 
-def dense_mask_min(n_items: int, d: int) -> int:
+def dense_mask_min(n_items: int, d: int, n_users: int = None) -> int:
+    if n_users is not None and n_users <= 256 * (256 if d <= 128 else 128):
+        return DENSE_MASK_MIN
     return max(DENSE_MASK_MIN, n_items * d // 32768)
 
 
@@ -163,7 +170,7 @@ class _Route:
         n = rows.numel()
         lens = (mask[0][1:] - mask[0][:-1]) if mask is not None else None
         heavy = torch.zeros(n, dtype=torch.bool, device=rows.device)
-        self.thr = dense_mask_min(n_items, d) if thr is None else thr
+        self.thr = dense_mask_min(n_items, d, n) if thr is None else thr
         if lens is not None and n_items <= DENSE_MAX_ITEMS:
             heavy = (lens > self.thr) & (lens <= n_items - k_max)
         self.n_heavy = int(heavy.sum())
