@@ -210,7 +210,8 @@ def make_step(A, E0, K, d, dtype, world, cfg, rank, timings):
         return step, A.nnz, A.n_rows
     # N > 1: A is this rank's shard (built from the edge list, never the full operator)
     shard = A
-    prop = ShardedPropagation(shard, E0[:cfg.n_users], E0[cfg.n_users:], K)
+    E0u, E0i = E0  # this rank's user rows, the full item table
+    prop = ShardedPropagation(shard, E0u, E0i, K, local_user_rows=True)
     models = {}
 
     # the N=1 conventions per shard operator: cache-aware model (hot set of the table it gathers),
@@ -256,7 +257,14 @@ def bench_propagation(args, rank, world, A, cfg, dtype, steps, warmup):
     dname = "bf16" if es == 2 else "f32"
     K, d = cfg.K, cfg.d
     N = cfg.n_users + cfg.n_items
-    E0 = lgx.fill_normal((N, d), 0.1, 2020, dtype=dtype)
+    if world == 1:
+        E0 = lgx.fill_normal((N, d), 0.1, 2020, dtype=dtype)
+    else:
+        # the rows of the N=1 table this rank reads: its own users (no replicated 10 M-row table)
+        # and the whole item table (the padded layer-0 item table every rank pulls from)
+        u0, u1 = int(A.user_bounds[rank]), int(A.user_bounds[rank + 1])
+        E0 = (lgx.fill_normal((u1 - u0, d), 0.1, 2020, dtype=dtype, first=u0 * d),
+              lgx.fill_normal((cfg.n_items, d), 0.1, 2020, dtype=dtype, first=cfg.n_users * d))
     timings = []
     step, local_nnz, _ = make_step(A, E0, K, d, dtype, world, cfg, rank, timings)
     nnz_all = local_nnz
@@ -315,12 +323,25 @@ def bench_propagation(args, rank, world, A, cfg, dtype, steps, warmup):
         mx = {n: max_over_ranks(float(ph.get(n, 0.0)), world) for n in names}
         out["comm_exposed_ms"] = mx.pop("comm_exposed_ms")
         out["phases_ms"] = mx
-        sync = ("; gloo has no device all-to-all: each exchange is a host-synchronous all-gather of the "
-                "slabs (exchange_sync), so this line is a rehearsal of the schedule, not of RCCL's overlap"
+        sync = ("; gloo has no device all-to-all: each exchange is a host-staged, host-synchronous "
+                "all-to-all (exchange_sync), so this line is a rehearsal of the schedule, not of RCCL's overlap"
                 if not step.prop._a2a_native else "")
         out["phases_note"] = (f"ms per step on the compute stream, max over {world} ranks; push in "
                               f"{len(step.prop.push_chunks)} chunks, each exchanged by its own all-to-all{sync}")
+        out["per_rank"] = gather_rank_stats(world, {
+            "rank": rank, "users": A.n_u_local, "pull_nnz": A.A_pull.nnz, "push_nnz": step.prop.push_nnz,
+            "peak_mem_gb": torch.cuda.max_memory_allocated() / 1e9,
+            "build_peak_mem_gb": getattr(A, "build_peak_gb", None), "build_s": getattr(A, "build_s", None),
+            "layer_launch_ms_mean": mean_launch_s * 1e3,
+            "kernel_ms_per_step": sum(v for kk, v in ph.items() if kk in ("push", "pull", "reduce", "epilogue"))})
     return out
+
+
+def gather_rank_stats(world: int, mine: dict) -> list:
+    """Every rank's dict on rank 0 (all_gather_object over the bench's group), in rank order."""
+    got = [None] * world
+    dist.all_gather_object(got, mine)
+    return got
 
 
 # ------------------------------------------------------------------------------------ CPU baseline
@@ -562,13 +583,29 @@ def main():
         A = synth_graph(cfg, seed=2020, device="cuda")
         log(f"[bench] graph {cfg.name}: N={cfg.n_users + cfg.n_items} nnz={A.nnz} built in {time.time() - t0:.1f}s")
     else:
-        # every rank draws the same seeded edge list and builds only its own rows
-        u, i = synth_edges(cfg, seed=2020, device="cuda")
-        A = make_shard_from_edges(u, i, cfg.n_users, cfg.n_items, rank, world)
-        del u, i
-        torch.cuda.empty_cache()
+        # every rank draws the same seeded edge list and builds only its own rows.  Ranks that share
+        # a GPU (one-GPU rehearsals) build one after another behind barriers, so that the edge
+        # draws' transient peaks (~30 GB at C4) do not coincide; on a node every rank has its own.
+        shared = world > max(1, torch.cuda.device_count())
+        A = None
+        for turn in range(world if shared else 1):
+            if not shared or turn == rank:
+                u, i = synth_edges(cfg, seed=2020, device="cuda")
+                A = make_shard_from_edges(u, i, cfg.n_users, cfg.n_items, rank, world)
+                del u, i
+                torch.cuda.synchronize()
+                torch.cuda.empty_cache()
+                print(f"[bench] rank {rank}: shard built ({time.time() - t0:.1f}s since start)",
+                      file=sys.stderr, flush=True)
+            if shared:
+                dist.barrier()
+        build_peak = torch.cuda.max_memory_allocated() / 1e9
+        A.build_peak_gb = build_peak
+        A.build_s = time.time() - t0
+        torch.cuda.reset_peak_memory_stats()
         log(f"[bench] shard {rank}/{world} of {cfg.name}: {A.n_u_local} users, pull nnz {A.A_pull.nnz} "
-            f"built in {time.time() - t0:.1f}s")
+            f"built in {time.time() - t0:.1f}s ({'rank-serialised' if shared else 'in parallel'}, "
+            f"build peak {build_peak:.1f} GB)")
     res = bench_propagation(args, rank, world, A, cfg, main_dtype, args.steps, args.warmup)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -598,7 +635,11 @@ def main():
                           else None),
         "roofline": res["roofline"], "cpu_baseline": cpu,
         **({"phases_ms": res["phases_ms"], "comm_exposed_ms": res["comm_exposed_ms"],
-            "phases_note": res["phases_note"]} if world > 1 else {}),
+            "phases_note": res["phases_note"], "per_rank": res["per_rank"],
+            "per_rank_note": "peak_mem_gb = torch.cuda.max_memory_allocated over the timed propagation (shard, "
+                             "tables, push chunks, exchange buffers; the shard build's transient peak is reset "
+                             "before it); kernel_ms_per_step = push + pull + reduce + epilogue on that rank"}
+           if world > 1 else {}),
         ("bf16" if extra and extra["dtype"] == "bf16" else "fp32"): extra,
         "scoring": scoring, "scoring_bf16": scoring16,
     }

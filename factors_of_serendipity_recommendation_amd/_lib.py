@@ -113,6 +113,7 @@ SIGNATURES = {
     "lgx_gather_scores": (_c_int, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp]),
     "lgx_synth_edges": (_c_int, [ctypes.c_uint64, _vp, _c_i64, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp]),
     "lgx_fill_normal": (_c_int, [_vp, _c_i64, ctypes.c_float, ctypes.c_uint64, _c_int, _vp]),
+    "lgx_fill_normal_at": (_c_int, [_vp, _c_i64, _c_i64, ctypes.c_float, ctypes.c_uint64, _c_int, _vp]),
 }
 
 _lib = None

@@ -129,16 +129,19 @@ __global__ void synth_edges_kernel(uint64_t seed, const int64_t* __restrict__ of
     items_out[e] = perm ? perm[lo] : (int32_t)lo;
 }
 
-__global__ void fill_normal_kernel(void* out, int64_t n, float std_, uint64_t seed, int dtype) {
-    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
+// element j of the output is element first + j of the seeded sequence (counter-based: any range of
+// the sequence is generated alone, so a rank fills only its own rows of a table)
+__global__ void fill_normal_kernel(void* out, int64_t first, int64_t n, float std_, uint64_t seed, int dtype) {
+    const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const int64_t i = first + j;
     const uint64_t h = splitmix64(seed ^ splitmix64((uint64_t)(i >> 1)));
     const float u1 = u01(h), u2 = u01(h << 24);
     const float r = sqrtf(-2.0f * logf(u1));
     const float z = (i & 1) ? r * sinf(6.283185307179586f * u2) : r * cosf(6.283185307179586f * u2);
     const float v = z * std_;
-    if (dtype == LGX_DTYPE_F32) static_cast<float*>(out)[i] = v;
-    else static_cast<uint16_t*>(out)[i] = f32_to_bf16(v);
+    if (dtype == LGX_DTYPE_F32) static_cast<float*>(out)[j] = v;
+    else static_cast<uint16_t*>(out)[j] = f32_to_bf16(v);
 }
 
 }  // namespace
@@ -214,11 +217,16 @@ extern "C" int lgx_synth_edges(uint64_t seed, const int64_t* user_offsets, int64
     return LGX_OK;
 }
 
-extern "C" int lgx_fill_normal(void* out, int64_t n, float std_, uint64_t seed, int dtype, lgx_stream_t stream) {
-    LGX_REQUIRE(out && n >= 0, LGX_ERR_INVALID_ARG, "lgx_fill_normal: bad arguments");
+extern "C" int lgx_fill_normal_at(void* out, int64_t first, int64_t n, float std_, uint64_t seed, int dtype,
+                                  lgx_stream_t stream) {
+    LGX_REQUIRE(out && n >= 0 && first >= 0, LGX_ERR_INVALID_ARG, "lgx_fill_normal: bad arguments");
     LGX_REQUIRE(dtype == LGX_DTYPE_F32 || dtype == LGX_DTYPE_BF16, LGX_ERR_INVALID_ARG, "lgx_fill_normal: dtype");
     if (n == 0) return LGX_OK;
-    fill_normal_kernel<<<ceil_div(n, 256), 256, 0, as_hip(stream)>>>(out, n, std_, seed, dtype);
+    fill_normal_kernel<<<ceil_div(n, 256), 256, 0, as_hip(stream)>>>(out, first, n, std_, seed, dtype);
     LGX_LAUNCH_CHECK();
     return LGX_OK;
+}
+
+extern "C" int lgx_fill_normal(void* out, int64_t n, float std_, uint64_t seed, int dtype, lgx_stream_t stream) {
+    return lgx_fill_normal_at(out, 0, n, std_, seed, dtype, stream);
 }

@@ -34,8 +34,8 @@ full tables).
 Diagnostics.  With record_phases set, every step stamps the compute stream after each phase
 (push, allgather_wait, pull, exchange_wait, reduce, epilogue); the waits are the time the stream
 sat behind a collective, i.e. the communication the schedule left exposed (phase_summary()).  Under
-gloo (CPU tests, one-GPU rehearsals) the exchange is a host-synchronous all-gather: its time is
-stamped as exchange_sync, and counts as exposed.
+gloo with device tensors (one-GPU rehearsals) the exchange is a host-staged, host-synchronous
+all-to-all: its time is stamped as exchange_sync, and counts as exposed.
 
 The SpMM and epilogue callables are injectable so that the CPU tests drive the same schedule over
 gloo with an oracle SpMM.
@@ -296,9 +296,12 @@ class ShardedPropagation:
     def __init__(self, shard: Shard, E0_user: torch.Tensor, E0_item: torch.Tensor, K: int,
                  group=None, layer_fn: Optional[LayerFn] = None, epilogue_fn: Optional[LayerFn] = None,
                  stack_fn: Optional[LayerFn] = None, force_collectives: bool = False,
-                 n_chunks: Optional[int] = None, sum_fn: Optional[Callable] = None):
+                 n_chunks: Optional[int] = None, sum_fn: Optional[Callable] = None,
+                 local_user_rows: bool = False):
         """E0_user / E0_item: the FULL layer-0 tables in global row order (replicated input, as every
-        rank holds the embedding parameters); dtype f32 or bf16.  The user side keeps its K-1 layer
+        rank holds the embedding parameters); dtype f32 or bf16.  local_user_rows: E0_user holds only
+        this rank's users [user_bounds[rank], user_bounds[rank+1]) -- the propagation never reads
+        another rank's user rows, so a caller need not hold the full [U, d] table (C4 fp32: 5.1 GB).  The user side keeps its K-1 layer
         tables and forms the mean in the last pull (stack_fn = lgx_propagate_layer_stack), as the
         single-GPU lgx_propagate does; the item side keeps the f32 running sum of its own block.
 
@@ -322,7 +325,12 @@ class ShardedPropagation:
         dev, dt = E0_user.device, E0_user.dtype
         u0, u1 = int(s.user_bounds[s.rank]), int(s.user_bounds[s.rank + 1])
         i0, i1 = int(s.item_bounds[s.rank]), int(s.item_bounds[s.rank + 1])
-        self.E0u = E0_user[u0:u1].contiguous()
+        if local_user_rows:
+            if E0_user.shape[0] != u1 - u0:
+                raise ValueError(f"ShardedPropagation: local_user_rows expects {u1 - u0} rows, got {E0_user.shape[0]}")
+            self.E0u = E0_user.contiguous()
+        else:
+            self.E0u = E0_user[u0:u1].contiguous()
         self.E0i = E0_item[i0:i1].contiguous()
         # users: local rows only, layers 0..K-1 kept; items: full padded tables, layer ping-pong
         self.Xu = [self.E0u] + [torch.zeros((s.n_u_local, d), dtype=dt, device=dev) for _ in range(max(1, K - 1))]
@@ -335,7 +343,7 @@ class ShardedPropagation:
         self.out_u = torch.zeros((s.n_u_local, d), dtype=torch.float32, device=dev)
         self.out_i = torch.zeros((s.n_i_local, d), dtype=torch.float32, device=dev)
         self._collective = s.world > 1 or force_collectives
-        # gloo has no all-to-all of device tensors: an all-gather of the slabs there (tests and
+        # gloo has no all-to-all of device tensors: staged through host tensors there (tests and
         # rehearsals only), the same slabs in the same order, hence the same sums
         self._a2a_native = self._collective and not (dev.type == "cuda" and dist.get_backend(group) == "gloo")
         if n_chunks is None:
@@ -376,10 +384,11 @@ class ShardedPropagation:
             return None
         if self._a2a_native:
             return dist.all_to_all_single(R, P, group=self.group, async_op=True)
-        w, r = self.s.world, self.s.rank
-        allp = torch.empty((w * w * m, self.d), dtype=P.dtype, device=P.device)
-        dist.all_gather_into_tensor(allp, P.reshape(w * m, self.d), group=self.group)
-        R.copy_(allp.view(w, w, m, self.d)[:, r])
+        # gloo with device tensors (rehearsals): the same all-to-all through host buffers, blocking;
+        # each rank moves the bytes RCCL would move, not the world-fold of an all-gather
+        Rh = torch.empty(R.shape, dtype=R.dtype)
+        dist.all_to_all_single(Rh, P.cpu(), group=self.group)
+        R.copy_(Rh)
         return None
 
     def _reduce(self, c0: int, m: int) -> None:

@@ -131,15 +131,20 @@ def check_pair(Q: torch.Tensor, items: torch.Tensor) -> None:
 
 
 def score_dense(Q: torch.Tensor, items: torch.Tensor, user_rows: Optional[torch.Tensor] = None,
-                apply_sigmoid: bool = False) -> torch.Tensor:
-    """[B, I] scores (getUsersRating, model.py:179-184 / TF batch_ratings, LightGCN.py:148)."""
+                apply_sigmoid: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[B, I] scores (getUsersRating, model.py:179-184 / TF batch_ratings, LightGCN.py:148); out: an
+    optional contiguous f32 [B, I] destination."""
     require_gpu(Q, items, user_rows)
     check_pair(Q, items)
     Q = Q.contiguous()
     items = items.contiguous()
     B = user_rows.numel() if user_rows is not None else Q.shape[0]
     rows = user_rows.to(torch.int64).contiguous() if user_rows is not None else None
-    out = torch.empty((B, items.shape[0]), dtype=torch.float32, device=Q.device)
+    if out is None:
+        out = torch.empty((B, items.shape[0]), dtype=torch.float32, device=Q.device)
+    elif (out.dtype != torch.float32 or tuple(out.shape) != (B, items.shape[0]) or not out.is_contiguous()
+          or out.device != Q.device):
+        raise ValueError(f"score_dense: out must be a contiguous float32 [{B}, {items.shape[0]}] on {Q.device}")
     _lib.check(_lib.lib().lgx_score_dense(Q.data_ptr(), _ptr(rows), items.data_ptr(), B, items.shape[0], Q.shape[1],
                                           _dtype_code(Q), int(apply_sigmoid), out.data_ptr(),
                                           _stream_ptr(Q.device)), "lgx_score_dense")
@@ -290,7 +295,8 @@ def dense_chunk_users(n_items: int, chunk_bytes: int = DENSE_CHUNK_BYTES) -> int
 
 def score_topk_dense_masked(Q: torch.Tensor, items: torch.Tensor, k: int, user_rows: torch.Tensor,
                             mask: Tuple[torch.Tensor, torch.Tensor], chunk_bytes: int = DENSE_CHUNK_BYTES,
-                            offsets: Optional[Sequence[torch.Tensor]] = None) -> torch.Tensor:
+                            offsets: Optional[Sequence[torch.Tensor]] = None,
+                            scratch: Optional[torch.Tensor] = None) -> torch.Tensor:
     """The ranking score_topk returns (idx int32 [B, k]; raw scores ranked, ties to the lower item id)
     by another route, for users whose mask is long: their dense raw score rows (lgx_score_dense), the
     masked entries set to -inf, the row top-k (lgx_topk_rows).  In the fused walk every masked item
@@ -298,14 +304,19 @@ def score_topk_dense_masked(Q: torch.Tensor, items: torch.Tensor, k: int, user_r
     saturated); here a mask costs one scattered store per item.  Every user must keep at least k
     unmasked items (the fused path's masked tail is not reproduced).  Users go in chunks of at most
     chunk_bytes of scores; offsets: the chunks' dense_mask_offsets, precomputed by a caller that ranks
-    the same users again (no host synchronisation then)."""
+    the same users again (no host synchronisation then); scratch: a flat f32 buffer of at least
+    min(B, chunk users) * n_items elements for the score chunks (a caller on a side stream allocates it
+    on its own stream, so the block returns to that stream's pool), else allocated here."""
     require_gpu(Q, items, user_rows)
     B, I = user_rows.numel(), items.shape[0]
     idx = torch.empty((B, k), dtype=torch.int32, device=Q.device)
     step = dense_chunk_users(I, chunk_bytes)
+    if scratch is not None and scratch.numel() < min(B, step) * I:
+        raise ValueError("score_topk_dense_masked: scratch holds fewer than one chunk of scores")
     for j, c0 in enumerate(range(0, B, step)):
         c1 = min(B, c0 + step)
-        S = score_dense(Q, items, user_rows=user_rows[c0:c1])
+        S = score_dense(Q, items, user_rows=user_rows[c0:c1],
+                        out=scratch[:(c1 - c0) * I].view(c1 - c0, I) if scratch is not None else None)
         off = offsets[j] if offsets is not None else dense_mask_offsets(mask, I, c0, c1)
         S.view(-1).index_fill_(0, off, float("-inf"))
         idx[c0:c1] = topk_rows(S, k)[0]
@@ -400,13 +411,23 @@ def test_metrics(rankings: torch.Tensor, truth: Tuple[torch.Tensor, torch.Tensor
     """Procedure.Test's metric sums over all users (Procedure.py:60-72, ``lgx_test_metrics``): rankings
     int32 [users, max(topks)], truth = sorted deduplicated test lists as a CSR, test_len = the lists'
     lengths with duplicates (int64 [users]) -> f64 [3, len(topks)] on the device: per topk the sums of
-    recall, of right (precision * topk) and of ndcg, in the order of ``topks``."""
+    recall, of right (precision * topk) and of ndcg, in the order of ``topks``.  Any number of topks
+    (the reference's list has no limit): the library takes 8 per launch, so longer lists go in groups."""
     require_gpu(rankings)
     r = rankings.to(torch.int32).contiguous()
     users, k = r.shape
     ks = [int(x) for x in topks]
-    if not ks or len(ks) > 8 or min(ks) < 1 or max(ks) != k:
-        raise ValueError(f"test_metrics: topks {ks} with rankings of width {k} (1..8 topks, max = width)")
+    if not ks or min(ks) < 1 or max(ks) != k:
+        raise ValueError(f"test_metrics: topks {ks} with rankings of width {k} (each in 1..width, max = width)")
+    if len(ks) > 8:
+        parts = [_test_metrics_group(r, truth, ks[g:g + 8], test_len) for g in range(0, len(ks), 8)]
+        return torch.cat(parts, dim=1)
+    return _test_metrics_group(r, truth, ks, test_len)
+
+
+def _test_metrics_group(r: torch.Tensor, truth, ks, test_len) -> torch.Tensor:
+    """test_metrics for at most 8 topks, each in [1, width] (the lgx_test_metrics contract)."""
+    users, k = r.shape
     order = sorted(range(len(ks)), key=lambda i: ks[i])
     tk = _device_const(("topks", tuple(ks[i] for i in order), str(r.device)),
                        lambda: torch.tensor([ks[i] for i in order], dtype=torch.int32, device=r.device))
@@ -451,11 +472,14 @@ def gather_scores(emb_user: torch.Tensor, emb_item: torch.Tensor, cand: Tuple[to
     return out[:n_pairs]
 
 
-def fill_normal(shape, std: float, seed: int, dtype=torch.float32, device="cuda") -> torch.Tensor:
+def fill_normal(shape, std: float, seed: int, dtype=torch.float32, device="cuda", first: int = 0) -> torch.Tensor:
+    """Deterministic N(0, std^2) table; `first` = flat offset into the seeded sequence, so
+    fill_normal((r1 - r0, d), ..., first=r0 * d) equals rows [r0, r1) of the full table."""
     t = torch.empty(shape, dtype=dtype, device=device)
     require_gpu(t)
-    _lib.check(_lib.lib().lgx_fill_normal(t.data_ptr(), t.numel(), float(std), int(seed) & (2**64 - 1),
-                                          _dtype_code(t), _stream_ptr(t.device)), "lgx_fill_normal")
+    _lib.check(_lib.lib().lgx_fill_normal_at(t.data_ptr(), int(first), t.numel(), float(std),
+                                             int(seed) & (2**64 - 1), _dtype_code(t), _stream_ptr(t.device)),
+               "lgx_fill_normal")
     return t
 
 

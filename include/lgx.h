@@ -282,10 +282,14 @@ int lgx_column_mean_f32(const float* src, int64_t rows, int64_t cols, float* out
  * rankings [users, k] int32 (k = max topks), test lists as a CSR with each list sorted ascending
  * (truth_indptr [users+1] int64, truth_indices int32, sorted and deduplicated), test_len [users] int64
  * = len(test list) with duplicates (nullable: the CSR lengths), topks [n_topks] int32 ascending in [1, k]
- * (n_topks <= 8), inv_log2 [k] f64 = 1/log2(j+2) -> sums [3, n_topks] f64 = per topk the sums over
- * users of right/|test| (recall), right (precision: divide by the topk) and dcg/idcg (ndcg, idcg over
- * min(topk, |test|) ranks, idcg == 0 -> 1, NaN -> 0).  Summed in a fixed order; workspace from
- * lgx_test_metrics_workspace.
+ * (n_topks <= 8), inv_log2 [k] f64 = 1/log2(j+2) -> sums [n_topks, 3] f64, row t = the sums over users
+ * for topks[t] of right/|test| (recall), right (precision: divide by the topk) and dcg/idcg (ndcg, idcg
+ * over min(topk, |test|) ranks, idcg == 0 -> 1, NaN -> 0): sums[3*t + 0 / 1 / 2].  Summed in a fixed
+ * order; workspace from lgx_test_metrics_workspace.
+ * Caller contract: topks lives on the device, so the library cannot check it without a host
+ * synchronisation: it must be ascending with every entry in [1, k]; an entry outside that range sums
+ * to zero.  More than 8 topks: call once per group of 8 (factors_of_serendipity_recommendation_amd/
+ * ops.py test_metrics does).
  */
 int lgx_test_metrics_workspace(int64_t users, int n_topks, size_t* bytes);
 int lgx_test_metrics(const int32_t* rankings, int64_t users, int k, const int64_t* truth_indptr,
@@ -439,6 +443,10 @@ int lgx_synth_edges(uint64_t seed, const int64_t* user_offsets, int64_t n_users,
                     int64_t n_edges, int32_t* users_out, int32_t* items_out, lgx_stream_t stream);
 /* Deterministic N(0, std^2) fill (Box-Muller over a counter hash), dtype f32 or bf16. */
 int lgx_fill_normal(void* out, int64_t n, float std, uint64_t seed, int dtype, lgx_stream_t stream);
+/* Elements [first, first + n) of the same sequence into out[0, n): a rank fills only its own rows of a
+ * table that lgx_fill_normal would fill whole (multi-GPU bench: no replicated [N, d] table). */
+int lgx_fill_normal_at(void* out, int64_t first, int64_t n, float std, uint64_t seed, int dtype,
+                       lgx_stream_t stream);
 
 #ifdef __cplusplus
 }

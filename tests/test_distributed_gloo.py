@@ -100,8 +100,8 @@ def test_sharded_propagation_gloo(world, K):
 
 
 def _chunk_worker(rank, world, port, K, result_q):
-    """One graph, the same shard, propagated with 1 / 3 / 4 / 7 push chunks: gathered outputs equal
-    bit for bit (each row keeps its summation; the cross-rank sum runs in rank order); phases
+    """One graph, the same shard, propagated with 1 / 3 / 4 / 7 push chunks and from the rank's own
+    user rows only: gathered outputs equal bit for bit (each row keeps its summation; the cross-rank sum runs in rank order); phases
     recorded for every step."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -116,14 +116,17 @@ def _chunk_worker(rank, world, port, K, result_q):
         E0 = torch.from_numpy((rng.standard_normal((U + I, 8)) * 0.1).astype(np.float32))
         shard = make_shard(A, U, I, rank, world, seg_len=16)
         outs, phases = [], None
-        for nc in (1, 3, 4, 7):
-            prop = ShardedPropagation(shard, E0[:U], E0[U:], K, layer_fn=cpu_layer, epilogue_fn=cpu_epilogue,
-                                      stack_fn=cpu_stack, n_chunks=nc)
+        u0, u1 = int(shard.user_bounds[rank]), int(shard.user_bounds[rank + 1])
+        for nc, local in ((1, False), (3, False), (4, False), (7, False), (4, True)):
+            # the last pass hands the rank only its own user rows (the bench's layout)
+            prop = ShardedPropagation(shard, E0[u0:u1] if local else E0[:U], E0[U:], K, layer_fn=cpu_layer,
+                                      epilogue_fn=cpu_epilogue, stack_fn=cpu_stack, n_chunks=nc,
+                                      local_user_rows=local)
             assert len(prop.push_chunks) == min(nc, shard.mi)
-            prop.record_phases = nc == 4
+            prop.record_phases = nc == 4 and not local
             prop.step()
             prop.step()
-            if nc == 4:
+            if prop.record_phases:
                 phases = prop.phase_summary()
             ou, oi = prop.gather_outputs()
             outs.append(torch.cat([ou, oi]).numpy())

@@ -47,9 +47,13 @@ def _worker(rank, world, port, K, dtype_name, q, backend="gloo"):
             E0 = E0.to(torch.bfloat16).float()
         shard = make_shard(A, U, I, rank, world, seg_len=64)
         outs = []
-        for nc in (1, 4):  # one push launch, then 4 chunks each with its own exchange
-            prop = ShardedPropagation(shard, E0[:U].cuda().to(dtype), E0[U:].cuda().to(dtype), K,
-                                      force_collectives=backend == "nccl", n_chunks=nc)
+        u0, u1 = int(shard.user_bounds[rank]), int(shard.user_bounds[rank + 1])
+        # one push launch, then 4 chunks each with its own exchange, then 4 chunks from this rank's
+        # user rows only (the bench's layout: no replicated user table)
+        for nc, local in ((1, False), (4, False), (4, True)):
+            Eu = E0[u0:u1] if local else E0[:U]
+            prop = ShardedPropagation(shard, Eu.cuda().to(dtype), E0[U:].cuda().to(dtype), K,
+                                      force_collectives=backend == "nccl", n_chunks=nc, local_user_rows=local)
             if backend == "nccl":
                 assert prop._collective and prop._a2a_native  # async all_to_all_single / all_gather_into_tensor
             prop.record_phases = True
@@ -63,6 +67,7 @@ def _worker(rank, world, port, K, dtype_name, q, backend="gloo"):
             outs.append((ou.clone(), oi.clone()))
         torch.cuda.synchronize()
         assert all(torch.equal(a, b) for a, b in zip(outs[0], outs[1])), "chunked layer differs from one launch"
+        assert all(torch.equal(a, b) for a, b in zip(outs[1], outs[2])), "local user rows differ from the full table"
         if rank == 0:
             ref = oracle.propagate(A.indptr.cpu().numpy(), A.indices.cpu().numpy(), A.vals.cpu().numpy(),
                                    E0.numpy(), K)

@@ -227,7 +227,8 @@ def test_evaluator_route_splits_long_masks():
     assert torch.equal(idx[~heavy], ref[~heavy])  # the light users are the fused launch's own result
 
 
-@pytest.mark.parametrize("topks", [[20], [1, 5, 20], [20, 5], [100, 10, 50]])
+@pytest.mark.parametrize("topks", [[20], [1, 5, 20], [20, 5], [100, 10, 50],
+                                   [1, 2, 3, 5, 8, 10, 15, 20, 30, 40, 50]])
 def test_test_metrics_kernel_matches_host_restatement(topks):
     """lgx_test_metrics (Procedure.Test's getLabel + RecallPrecision_ATk + NDCGatK_r sums in one launch)
     against the host restatement of utils.py:218-285 on the same rankings: short and power-law test
@@ -261,3 +262,37 @@ def test_test_metrics_kernel_matches_host_restatement(topks):
     np.testing.assert_allclose(got[0], want["recall"], rtol=1e-12)
     np.testing.assert_allclose(got[1] / np.asarray(topks, dtype=float), want["precision"], rtol=1e-12)
     np.testing.assert_allclose(got[2], want["ndcg"], rtol=1e-12)
+
+
+def test_test_metrics_c_abi_layout_is_topk_major():
+    """lgx_test_metrics through the C ABI (as a C caller following include/lgx.h binds it), 2 topks:
+    sums[3*t + m] = metric m (recall, right, ndcg) of topks[t], i.e. [n_topks, 3]."""
+    import ctypes
+    from factors_of_serendipity_recommendation_amd import _lib
+    rng = np.random.default_rng(11)
+    n_users, n_items, topks = 500, 2000, [5, 20]
+    K = max(topks)
+    truths = [sorted(set(rng.choice(n_items, size=int(rng.integers(1, 40)), replace=False).tolist()))
+              for _ in range(n_users)]
+    rank = np.stack([rng.choice(n_items, size=K, replace=False) for _ in range(n_users)]).astype(np.int32)
+    for u in range(n_users):
+        rank[u, int(rng.integers(0, K))] = truths[u][0] if truths[u][0] not in rank[u] else rank[u, 0]
+    ip, ix = ops.lists_to_device_csr(truths, DEV, sort=True)
+    r = torch.from_numpy(rank).to(DEV)
+    tk = torch.tensor(topks, dtype=torch.int32, device=DEV)
+    tl = ops.inv_log2_table(K, DEV)
+    L = _lib.lib()
+    ws = ctypes.c_size_t(0)
+    _lib.check(L.lgx_test_metrics_workspace(n_users, len(topks), ctypes.byref(ws)), "ws")
+    work = torch.empty(max(ws.value, 8), dtype=torch.uint8, device=DEV)
+    sums = torch.full((len(topks) * 3,), float("nan"), dtype=torch.float64, device=DEV)
+    _lib.check(L.lgx_test_metrics(r.data_ptr(), n_users, K, ip.data_ptr(), ix.data_ptr(), None, tk.data_ptr(),
+                                  len(topks), tl.data_ptr(), sums.data_ptr(), work.data_ptr(), ws.value, None),
+               "lgx_test_metrics")
+    torch.cuda.synchronize()
+    got = sums.cpu().numpy().reshape(len(topks), 3)
+    hit = np.array([[x in set(t) for x in rank[u]] for u, t in enumerate(truths)], dtype=float)
+    want = evaluator._metrics(hit, np.array([len(t) for t in truths]), topks)
+    for t, k in enumerate(topks):
+        np.testing.assert_allclose(got[t], [want["recall"][t], want["precision"][t] * k, want["ndcg"][t]],
+                                   rtol=1e-12)

@@ -399,3 +399,26 @@ def test_eval_caches_see_in_place_edits_and_clear():
     assert y is not x and evaluator._BatchLists.get(users, train, test, 0, dev) is y
     evaluator.clear_caches()
     assert evaluator._BatchLists.get(users, train, test, 0, dev) is not y
+
+
+def test_batch_lists_cache_checks_every_user():
+    """The batch_test cache compares every user, not a sample: an in-place edit of the caller's user
+    list at any position (the same list object), or of an equal numpy array, rebuilds the lists."""
+    from factors_of_serendipity_recommendation_amd import evaluator
+    rng = np.random.default_rng(21)
+    train = {u: sorted(rng.choice(500, 6, replace=False).tolist()) for u in range(300)}
+    test = {u: sorted(rng.choice(500, 3, replace=False).tolist()) for u in range(300)}
+    dev = torch.device("cpu")
+    users = list(range(0, 200))
+    a = evaluator._BatchLists.get(users, train, test, 0, dev)
+    assert evaluator._BatchLists.get(users, train, test, 0, dev) is a
+    for pos in (1, 77, 133, 198):  # positions between the 32 sampled ones included
+        users[pos] = 250 + pos % 50
+        b = evaluator._BatchLists.get(users, train, test, 0, dev)
+        assert b is not a and b.rows.tolist() == users
+        a = b
+    arr = np.asarray(users, dtype=np.int64)
+    c = evaluator._BatchLists.get(arr, train, test, 0, dev)
+    assert evaluator._BatchLists.get(arr, train, test, 0, dev) is c
+    arr[101] = 299
+    assert evaluator._BatchLists.get(arr, train, test, 0, dev).rows.tolist() == arr.tolist()

@@ -5,7 +5,10 @@ STACK mean in the last pull), with the collectives stubbed out.  Prints one JSON
 per-rank phase times, the single-GPU step on the same graph, the collective volumes per layer, and
 a predicted step time and speedup at two assumed RCCL rates.
 
-  python tools/shard_probe.py [--world 8] [--ranks 0,7] [--dtype f32] [--reps 3] [--chunks 4]
+  python tools/shard_probe.py [--world 8] [--ranks all] [--dtype f32] [--reps 3] [--chunks 4] [--contend]
+
+--contend also times every rank with the collectives replaced by device copies of their bytes on a
+side stream (_CopyComm): the SpMM under the HBM traffic and CU use of the exchanges.
 """
 import argparse
 import json
@@ -38,6 +41,54 @@ class _NoComm(ShardedPropagation):
         return None
 
 
+class _Done:
+    """A collective handle whose wait() makes the compute stream wait for a side-stream event."""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+
+
+class _CopyComm(ShardedPropagation):
+    """The product schedule with every collective replaced by device copies of the bytes it moves
+    through this GPU's HBM, issued on a side stream at the collective's place in the schedule and
+    waited for where the collective is waited for: chunk c's all-to-all reads its [world, mc, d]
+    send slabs and writes the received ones (R <- P), the all-gather writes the world-1 peer blocks
+    of the padded item table.  The link time is not in it (no peer); the interference of that
+    traffic and of the copy kernels' CUs with the overlapped SpMM is."""
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self.side = torch.cuda.Stream()
+        self._a2a_native = True  # async handles, as RCCL's: no host-synchronous exchange stamps
+
+    def _side(self, fn):
+        ev = torch.cuda.Event()
+        ev.record()
+        self.side.wait_event(ev)
+        with torch.cuda.stream(self.side):
+            fn()
+            done = torch.cuda.Event()
+            done.record()
+        return _Done(done)
+
+    def _exchange(self, c0, m):
+        P, R = self._chunk_views(c0, m)
+        return self._side(lambda: R.copy_(P))
+
+    def _all_gather(self, table):
+        s = self.s
+        blocks = table.view(s.world, s.mi, self.d)
+
+        def fn():
+            for q in range(s.world):
+                if q != s.rank:
+                    blocks[q].copy_(self.send_i)
+        return self._side(fn)
+
+
 def timed_steps(fn, reps):
     fn()
     torch.cuda.synchronize()
@@ -55,7 +106,8 @@ def timed_steps(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=8)
-    ap.add_argument("--ranks", default="0,7")
+    ap.add_argument("--ranks", default="all")
+    ap.add_argument("--contend", action="store_true")
     ap.add_argument("--dtype", default="f32", choices=["bf16", "f32"])
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--chunks", type=int, default=4)
@@ -83,10 +135,21 @@ def main():
         torch.cuda.empty_cache()
     u, i = synth_edges(cfg, seed=2020, device="cuda")
     ranks = []
-    for r in (int(x) for x in args.ranks.split(",")):
+    rank_ids = range(w) if args.ranks == "all" else [int(x) for x in args.ranks.split(",")]
+    for r in rank_ids:
         t0 = time.time()
         sh = make_shard_from_edges(u, i, U, I, r, w)
         build = time.time() - t0
+        contended = None
+        if args.contend:
+            cp = _CopyComm(sh, E0[:U], E0[U:], K, force_collectives=True, n_chunks=args.chunks)
+            contended = timed_steps(cp.step, args.reps)
+            cp.record_phases = True
+            for _ in range(args.reps):
+                cp.step()
+            cph = cp.phase_summary()
+            del cp
+        torch.cuda.reset_peak_memory_stats()
         prop = _NoComm(sh, E0[:U], E0[U:], K, force_collectives=True, n_chunks=args.chunks)
         step_ms = timed_steps(prop.step, args.reps)
         prop.record_phases = True
@@ -99,12 +162,17 @@ def main():
         rec = {"rank": r, "users": sh.n_u_local, "pull_nnz": sh.A_pull.nnz, "push_nnz": sh.A_push.nnz,
                "push_chunks": len(prop.push_chunks), "shard_build_s": round(build, 2), "step_ms": step_ms,
                "phases_ms_per_step": {k: v for k, v in ph.items() if k in ("push", "pull", "reduce", "epilogue")},
-               "all_to_all_bytes_per_layer": int(a2a_bytes), "all_gather_bytes_per_layer": int(ag_bytes)}
+               "all_to_all_bytes_per_layer": int(a2a_bytes), "all_gather_bytes_per_layer": int(ag_bytes),
+               "peak_mem_gb_schedule": torch.cuda.max_memory_allocated() / 1e9}
+        if contended is not None:
+            rec["step_ms_with_copy_collectives"] = contended
+            rec["phases_ms_with_copy_collectives"] = {k: v for k, v in cph.items() if k != "begin"}
         ranks.append(rec)
         print(json.dumps(rec), file=sys.stderr, flush=True)
         del sh, prop
         torch.cuda.empty_cache()
     worst = max(ranks, key=lambda x: x["step_ms"])
+    worst_c = max(ranks, key=lambda x: x.get("step_ms_with_copy_collectives", 0.0))
     ph = worst["phases_ms_per_step"]
     push_l, pull_l = ph["push"] / K, ph["pull"] / K
     nch = worst["push_chunks"]
@@ -124,8 +192,17 @@ def main():
         pred[name] = {"per_peer_GBs_assumed": per_peer_gbs, "all_to_all_ms_per_layer": a2a,
                       "all_gather_ms_per_layer": ag, "exposed_comm_ms_per_step": exposed, "step_ms": step,
                       "speedup_vs_1gpu": (one_gpu / step) if one_gpu else None}
+        if "step_ms_with_copy_collectives" in worst_c:
+            # the slowest rank with the exchanges' HBM traffic and copy kernels running beside it
+            # (measured) plus the link time the windows do not cover (modelled as above)
+            step_c = worst_c["step_ms_with_copy_collectives"] + exposed
+            pred[name]["step_ms_with_copy_contention"] = step_c
+            pred[name]["speedup_vs_1gpu_with_copy_contention"] = (one_gpu / step_c) if one_gpu else None
     print(json.dumps({"workload": f"synth10m {args.dtype} K={K} d={d}, world={w}", "one_gpu_step_ms": one_gpu,
+                      "ranks_timed": [x["rank"] for x in ranks],
                       "ranks": ranks, "critical_rank": worst["rank"], "kernel_ms_per_step": worst["step_ms"],
+                      "kernel_ms_per_step_by_rank": [round(x["step_ms"], 3) for x in ranks],
+                      "critical_rank_with_copy_collectives": worst_c["rank"] if args.contend else None,
                       "prediction": pred,
                       "note": "per-rank kernels of ShardedPropagation.step (collectives stubbed out) timed on one "
                               "MI355X with HIP events, best of reps; collective times are volumes / assumed "
