@@ -84,8 +84,15 @@ def main():
                            "hbm_bytes_per_launch": (2 * f + w) * 1024}
     import hashlib
     h = hashlib.sha256(open(os.path.join(ROOT, "factors_of_serendipity_recommendation_amd", "liblgx.so"), "rb").read())
-    doc = {"workload": f"{config} (bench.py default: propagation K=3 d=128 f32 and bf16 + scoring d=256 f32 "
-                       "(262144 users) and bf16 (1M users), 1M items), n_gpus=1",
+    # the scoring legs' sizes as the profiled bench line reports them (not a hard-coded string)
+    legs = "scoring legs: see the bench line"
+    try:
+        line = json.load(open(os.path.join(src, "bench_under_rocprof.json")))
+        legs = "; ".join(f"scoring {x['dtype']} d={x['d']}: {x['users_per_step']} users x {x['n_items']} items"
+                         for x in (line.get("scoring"), line.get("scoring_bf16")) if x)
+    except (OSError, ValueError, KeyError, TypeError):
+        pass
+    doc = {"workload": f"{config} (bench.py: propagation K=3 d=128 f32 and bf16; {legs}), n_gpus=1",
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (tools/profile_round.sh); "
                      "bytes = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024, the x2 measured for streaming reads and for "
                      "random 256-B / 512-B row gathers (profiles/r02_fetch_calibration.json). FETCH_SIZE counts "
