@@ -796,16 +796,26 @@ __device__ __forceinline__ uint32_t lds_u32(const void* p) {
 // stagger (no partner wave to overlap), a 2-buffer ring of 64 KB tiles at d = 256.
 constexpr int kBf16LdsWaves = 8;
 constexpr int kF32LdsWaves = 4;
-template <int DT, int KSTEPS, bool MINMAX, int MODE, int WAVES, int NACC, bool STAGGER>
+// Producer / consumer walk (PC, fp32 at d = 64): WAVES = 8 waves, waves 0-3 consumers and 4-7
+// producers; consumer w and producer w + 4 share a SIMD and 32 users.  The producer streams the tiles
+// (LDS-DMA ring) and issues the MFMAs; it hands each tile's 32 x 64 scores, still in the MFMA layout,
+// to its consumer through an LDS score buffer (two slots per pair), and the consumer runs the top-k
+// epilogue, the mask and the exact path -- so a tile's events run on the SIMD beside the next tile's
+// MFMAs instead of after them.  One workgroup barrier per tile: producer p writes tile t - 1's scores
+// while it has tile t's MFMAs in flight, consumer p ranks tile t - 2.  SCORE_SLOT bytes per slot.
+constexpr int kPcScoreSlot = 8 * 1024;
+template <int DT, int KSTEPS, bool MINMAX, int MODE, int WAVES, int NACC, bool STAGGER, bool PC = false>
 __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreArgs a, int xcd_affine,
                                                     int64_t n_utiles, int nbuf) {
     constexpr bool F32 = DT == LGX_DTYPE_F32;
     static_assert(NACC == 2 && (F32 || KSTEPS % 2 == 0), "16x16 walk: 64-item tiles, bf16 d a multiple of 32");
+    static_assert(!PC || (F32 && WAVES == 8 && !STAGGER && !MINMAX && MODE != kMinMaxOnly), "PC: fp32 top-k / floor walk");
+    constexpr int UW = PC ? WAVES / 2 : WAVES;  // waves that own users (and their lists)
     // SKIP: the fast-path test runs on the MFMA output layout itself (lane l holds 16 scores of user
     // l & 15 and 16 of user 16 + (l & 15)); the regroup into the top-k layout (16 v_permlane16_swap)
     // is paid only by tiles that have a survivor.  Min / max needs every score: not with MINMAX.
     constexpr bool SKIP = !MINMAX && MODE == kTopK;
-    typedef LdsGeom<KSTEPS, WAVES, NACC, F32 ? 4 : 2> G;
+    typedef LdsGeom<KSTEPS, UW, NACC, F32 ? 4 : 2> G;  // USERS = UW x 32; PPW: pieces per staging wave
     typedef Frag<DT> F;
     constexpr int NS = G::CPR / 4;                  // 16x16 walk: chunk groups (k-steps of 4 chunks) per row
     constexpr int UFN = 2 * NS;                     // user fragment registers (16 B each)
@@ -814,8 +824,12 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5, col = lane & 31;
-    typedef WaveTopKT<lds_pend(F32, KSTEPS, WAVES)> TopK;
-    uint64_t* lk = reinterpret_cast<uint64_t*>(smem + (size_t)nbuf * G::TILE + (size_t)wave * list_bytes_per_wave(k, TopK::kPend));
+    const bool producer = PC && wave >= UW;  // wave-uniform
+    const int uwave = PC ? wave % UW : wave;  // the user block of this wave (its pair's, PC)
+    typedef WaveTopKT<lds_pend(F32, KSTEPS, PC ? UW : WAVES)> TopK;
+    unsigned char* sbuf_pc = smem + (size_t)nbuf * G::TILE;  // PC: [UW pairs][2 slots][kPcScoreSlot]
+    uint64_t* lk = reinterpret_cast<uint64_t*>(sbuf_pc + (PC ? (size_t)UW * 2 * kPcScoreSlot : 0) +
+                                               (size_t)uwave * list_bytes_per_wave(k, TopK::kPend));
 
     // workgroup -> (catalog split, user tile)
     const int64_t bid = blockIdx.x;
@@ -832,26 +846,28 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     }
     if (utile >= n_utiles) return;
 
-    const int64_t b = utile * G::USERS + wave * kUsersPerWave + col;
+    const int64_t b = utile * G::USERS + uwave * kUsersPerWave + col;
     const bool user_ok = b < a.B;
     uint4 uf[UFN];
     const int r16 = lane & 15, q4 = lane >> 4;
     // B fragment (ub, s) at uf[ub * NS + s]: user 16 ub + r16, 16-B chunk 4 s + q4 of its row
 #pragma unroll
     for (int ub = 0; ub < 2; ++ub) {
-        const int64_t bu = utile * G::USERS + wave * kUsersPerWave + 16 * ub + r16;
-        const bool ok = bu < a.B;
+        const int64_t bu = utile * G::USERS + uwave * kUsersPerWave + 16 * ub + r16;
+        const bool ok = bu < a.B && !(PC && !producer);  // PC: only producers hold the users' rows
         const int64_t qr = ok ? (a.user_rows ? a.user_rows[bu] : bu) : 0;
 #pragma unroll
         for (int s2 = 0; s2 < NS; ++s2)
             uf[ub * NS + s2] = __builtin_bit_cast(uint4, F::load(a.Q, qr, a.d, 2 * s2 + (q4 >> 1), q4 & 1, ok));
     }
     TopK st;
-    st.init(lk, lk + list_keys_per_wave(k), k, lane, b, user_ok);
-    st.enable_suspects(a, split);
-    st.build_bloom(a);
-    if (a.seed_score) st.seed(a);
-    else if (MODE != kFloorOnly && a.floor && user_ok) st.tau = a.floor[b * a.n_splits + split];
+    st.init(lk, lk + list_keys_per_wave(k), k, lane, b, user_ok && !producer);
+    if (!producer) {
+        st.enable_suspects(a, split);
+        st.build_bloom(a);
+        if (a.seed_score) st.seed(a);
+        else if (MODE != kFloorOnly && a.floor && user_ok) st.tau = a.floor[b * a.n_splits + split];
+    }
     // consume the prologue loads here: otherwise the compiler treats them as possibly pending at
     // the loop header and waits vmcnt(0) -- i.e. for the tile prefetch -- in every iteration
 #pragma unroll
@@ -875,7 +891,8 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     // row q / CPR, fetched from source chunk (q % CPR) ^ (row & SWZ) (the swizzle lives on the source
     // side because the DMA's LDS destination is lane-linear)
     constexpr int PPW = G::PPW;
-    const int my_pieces = max(0, min(PPW, G::PIECES - wave * PPW));
+    const int swave = PC ? (producer ? uwave : UW) : wave;  // staging index (PC consumers stage nothing)
+    const int my_pieces = max(0, min(PPW, G::PIECES - swave * PPW));
     const uint32_t lds_tiles = lds_u32(tiles);
 
     auto tile_start = [&](int64_t t) {
@@ -893,12 +910,12 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
             const bool tail = t0 + G::TILE_ITEMS > i_end;
             const int last = (int)(i_end - 1 - t0);  // tail rows re-read the split's last row (masked later)
             // offsets recomputed per tile: cheaper than holding them in registers
-            const int q = (wave * PPW + p) * 64 + lane;
+            const int q = (swave * PPW + p) * 64 + lane;
             const int row = q / G::CPR;
             const int src = (q % G::CPR) ^ (row & G::SWZ);
             const int srow = tail && row > last ? last : row;
             lds_dma16(base, (uint32_t)(srow * G::RB + src * 16),
-                      __builtin_amdgcn_readfirstlane(lds_tiles + buf * G::TILE + (wave * PPW + p) * 1024));
+                      __builtin_amdgcn_readfirstlane(lds_tiles + buf * G::TILE + (swave * PPW + p) * 1024));
         }
     };
     auto stage = [&](int buf, int64_t t0) {
@@ -943,14 +960,15 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
             }
         }
     };
-    // scores of the tile in ring buffer `buf` into acc0 / acc1 (the same code for both wave kinds)
-    auto compute = [&]() {
+    // scores of the tile in ring buffer `buf` into cc (c, or a PC producer's own pair of sets); with
+    // MINMAX top-k also into acc0 / acc1 (the same code for both wave kinds)
+    auto compute_into = [&](f32x4 (&cc)[2][4]) {
         const unsigned char* T = tiles + buf * G::TILE;
         constexpr int KS2 = NS;
 #pragma unroll
         for (int ub = 0; ub < 2; ++ub)
 #pragma unroll
-            for (int ib = 0; ib < 4; ++ib) c[ub][ib] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            for (int ib = 0; ib < 4; ++ib) cc[ub][ib] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         // A fragment (s, ib): item 16 ib + r16, source chunk 4 s + q4 (LDS chunk ^ row swizzle)
         const unsigned char* rowp = T + r16 * G::RB;
         auto frag = [&](int s2, int ib) {
@@ -970,14 +988,14 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
                     if constexpr (F32) {
                         const float4 av = __builtin_bit_cast(float4, fa[ib]);
                         const float4 bv = __builtin_bit_cast(float4, uf[ub * KS2 + s2]);
-                        c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, c[ub][ib], 0, 0, 0);
-                        c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, c[ub][ib], 0, 0, 0);
-                        c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, c[ub][ib], 0, 0, 0);
-                        c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, c[ub][ib], 0, 0, 0);
+                        cc[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, cc[ub][ib], 0, 0, 0);
+                        cc[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, cc[ub][ib], 0, 0, 0);
+                        cc[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, cc[ub][ib], 0, 0, 0);
+                        cc[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, cc[ub][ib], 0, 0, 0);
                     } else {
-                        c[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        cc[ub][ib] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                             __builtin_bit_cast(bf16x8, fa[ib]), __builtin_bit_cast(bf16x8, uf[ub * KS2 + s2]),
-                            c[ub][ib], 0, 0, 0);
+                            cc[ub][ib], 0, 0, 0);
                     }
                 }
                 if (s2 + 1 < KS2) fa[ib] = frag(s2 + 1, ib);
@@ -994,11 +1012,12 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         }
         if (!SKIP && MODE == kTopK) regroup();
     };
+    auto compute = [&]() { compute_into(c); };
     // the split's last tile is the only one that can run past i_end: a block variant of its own
     // min / max mode: every score of the tile straight from the MFMA layout.  Rows past the split's
     // end re-read its last item (stage_piece), so they hold real scores; padding users do not.
-    const bool uok0 = utile * G::USERS + wave * kUsersPerWave + r16 < a.B;
-    const bool uok1 = utile * G::USERS + wave * kUsersPerWave + 16 + r16 < a.B;
+    const bool uok0 = utile * G::USERS + uwave * kUsersPerWave + r16 < a.B;
+    const bool uok1 = utile * G::USERS + uwave * kUsersPerWave + 16 + r16 < a.B;
     auto minmax_tile = [&]() {
         float lo0 = c[0][0][0], hi0 = c[0][0][0], lo1 = c[1][0][0], hi1 = c[1][0][0];
 #pragma unroll
@@ -1113,6 +1132,45 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     // a VALU phase: MI355X_MICROARCH.md).  Either way it lands in the buffer every wave released at
     // the previous barrier, and before this iteration's vmcnt wait.
     const bool stage_after = STAGGER && !late;  // wave-uniform
+    if constexpr (PC) {
+        // slot s of pair uwave: 8 lane-linear 16-B chunks per lane, c[ub][ib] at chunk 4 ub + ib
+        auto slot = [&](int64_t t) { return sbuf_pc + ((size_t)uwave * 2 + (size_t)(t & 1)) * kPcScoreSlot + lane * 16; };
+        // producer: tile t into one register set while the other (tile t - 1, its MFMAs issued an
+        // iteration ago) goes to the score buffer -- no wait on this tile's MFMAs before the barrier
+        f32x4 cA[2][4], cB[2][4];
+        auto iter = [&](int64_t t, f32x4 (&cur)[2][4], f32x4 (&prev)[2][4]) {
+            if (producer) {
+                if (t > 0 && t <= ntiles) {
+                    unsigned char* sp = slot(t - 1);
+#pragma unroll
+                    for (int ub = 0; ub < 2; ++ub)
+#pragma unroll
+                        for (int ib = 0; ib < 4; ++ib)
+                            *reinterpret_cast<f32x4*>(sp + (4 * ub + ib) * 1024) = prev[ub][ib];
+                }
+                if (t < ntiles) {
+                    if (t + ahead < ntiles) stage(sbuf, tile_start(t + ahead));
+                    compute_into(cur);
+                }
+                wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(t + ahead, ntiles - 1) - (t + 1)));
+            } else if (t >= 2) {  // tile t - 2, published by the previous barrier
+                const unsigned char* sp = slot(t - 2);
+#pragma unroll
+                for (int ub = 0; ub < 2; ++ub)
+#pragma unroll
+                    for (int ib = 0; ib < 4; ++ib) c[ub][ib] = *reinterpret_cast<const f32x4*>(sp + (4 * ub + ib) * 1024);
+                epilogue(tile_start(t - 2));
+            }
+            __syncthreads();
+            buf = buf + 1 == nbuf ? 0 : buf + 1;
+            sbuf = sbuf + 1 == nbuf ? 0 : sbuf + 1;
+        };
+        for (int64_t t = 0; t < ntiles + 2; t += 2) {
+            iter(t, cA, cB);
+            if (t + 1 < ntiles + 2) iter(t + 1, cB, cA);
+        }
+        if (producer) return;
+    } else
     for (int64_t t = 0; t < ntiles; ++t) {
         const int64_t t0 = tile_start(t);
         if (!stage_after && t + ahead < ntiles) stage(sbuf, tile_start(t + ahead));
@@ -1143,7 +1201,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     if constexpr (MODE == kFloorOnly) {
 #pragma unroll
         for (int ub = 0; ub < 2; ++ub) {
-            const int64_t bu = utile * G::USERS + wave * kUsersPerWave + 16 * ub + r16;
+            const int64_t bu = utile * G::USERS + uwave * kUsersPerWave + 16 * ub + r16;
             const bool ok = bu < a.B;
             // drop the groups that hold a masked item of the user (the mask rows are sorted)
             if (a.mask_indptr && ok) {
@@ -1210,6 +1268,14 @@ void score_topk_f32_lds(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     score_topk_lds_body<LGX_DTYPE_F32, KSTEPS, MINMAX, MODE, WAVES, 2, (WAVES > 4)>(
         smem, a, xcd_affine, n_utiles, nbuf);
+}
+
+// the producer / consumer walk (PC) for fp32 d = 64: 4 consumer + 4 producer waves, 128 users
+template <int KSTEPS, int MODE = 0>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void score_topk_f32_pc(ScoreArgs a, int xcd_affine, int64_t n_utiles, int nbuf) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    score_topk_lds_body<LGX_DTYPE_F32, KSTEPS, false, MODE, 8, 2, false, true>(smem, a, xcd_affine, n_utiles, nbuf);
 }
 
 __global__ void minmax_finish(const uint32_t* mm, float* out) {
@@ -1862,6 +1928,33 @@ int launch_f32_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t st
     return LGX_OK;
 }
 
+// the producer / consumer walk replaces the 4-wave fp32 walk at d = 64 (the top-k sweep)
+// where two ring tiles, the score buffers and the 4 consumers' lists fit the LDS (k <= 24 at 16 slots)
+inline bool f32_pc(const SplitPlan& p, int64_t d, int k, bool mm) {
+    return p.waves == kF32LdsWaves && d == 64 && !mm &&
+           2 * (size_t)kTileItems * 64 * 4 + (size_t)kF32LdsWaves * 2 * kPcScoreSlot +
+                   (size_t)kF32LdsWaves * list_bytes_per_wave(k, lds_pend(true, 4, kF32LdsWaves)) <= kLdsBytes;
+}
+
+template <int KS, int MODE>
+int launch_f32_pc_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream) {
+    typedef LdsGeom<KS, kF32LdsWaves, 2, 4> G;
+    const size_t lists = (size_t)kF32LdsWaves * list_bytes_per_wave(a.k, lds_pend(true, KS, kF32LdsWaves));
+    const size_t sb = (size_t)kF32LdsWaves * 2 * kPcScoreSlot;
+    const int nbuf = lds_ring_buffers(G::TILE, lists + sb, 1);
+    const size_t shmem = (size_t)nbuf * G::TILE + sb + lists;
+    if (shmem > kLdsBytes) {
+        set_error("lgx_score_topk: f32 producer/consumer kernel needs %zu B of LDS", shmem);
+        return LGX_ERR_UNSUPPORTED;
+    }
+    int rc = set_lds_limit(score_topk_f32_pc<KS, MODE>, shmem);
+    if (rc) return rc;
+    const unsigned grid = (unsigned)(p.n_utiles * p.n_splits);
+    score_topk_f32_pc<KS, MODE><<<grid, 512, shmem, stream>>>(a, p.xcd_affine ? 1 : 0, p.n_utiles, nbuf);
+    LGX_LAUNCH_CHECK();
+    return LGX_OK;
+}
+
 template <bool MM, int MODE = kTopK>
 int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream, int dtype = LGX_DTYPE_BF16) {
     const int ksteps = (int)(a.d / 16);
@@ -1876,6 +1969,8 @@ int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream, int d
                         return LGX_ERR_UNSUPPORTED;
                 }
             }
+            if constexpr (!MM && MODE == kTopK)  // the floor pass keeps the 4-wave walk (its maxima spill here)
+                if (f32_pc(p, a.d, a.k, MM)) return launch_f32_pc_kernel<4, MODE>(a, p, stream);
             switch (ksteps) {
                 case 4: return launch_f32_lds_kernel<4, MM, MODE>(a, p, stream);
                 case 8: return launch_f32_lds_kernel<8, MM, MODE>(a, p, stream);
@@ -2020,7 +2115,8 @@ extern "C" int lgx_score_topk_plan(int64_t B, int64_t n_items, int64_t d, int dt
     for (int i = 0; i < n && off < len; ++i) {
         const SplitPlan& p = r[i].p;
         const char* kern = p.lds ? (dtype == LGX_DTYPE_F32 ? (p.waves == 8 ? "score_topk_f32_lds<8 waves, 64-item tiles, 16x16x4>"
-                                                                            : "score_topk_f32_lds<4 waves, 64-item tiles, 16x16x4>")
+                                                              : f32_pc(p, d, k, false) ? "score_topk_f32_lds<4 waves + 4 producers, 64-item tiles, 16x16x4>"
+                                                                                    : "score_topk_f32_lds<4 waves, 64-item tiles, 16x16x4>")
                                                            : "score_topk_bf16_lds<8 waves, 64-item tiles, 16x16x32>")
                                  : (v1_waves(k) == 4 ? "score_topk_kernel<4 waves>" : "score_topk_kernel<1 wave>");
         const char* mode = p.lds ? (p.n_splits == 1 ? "full-sweep" : (p.xcd_affine ? "split-xcd" : "split"))

@@ -477,9 +477,12 @@ def fill_normal(shape, std: float, seed: int, dtype=torch.float32, device="cuda"
     fill_normal((r1 - r0, d), ..., first=r0 * d) equals rows [r0, r1) of the full table."""
     t = torch.empty(shape, dtype=dtype, device=device)
     require_gpu(t)
-    _lib.check(_lib.lib().lgx_fill_normal_at(t.data_ptr(), int(first), t.numel(), float(std),
-                                             int(seed) & (2**64 - 1), _dtype_code(t), _stream_ptr(t.device)),
-               "lgx_fill_normal")
+    L, sd = _lib.lib(), int(seed) & (2**64 - 1)
+    rc = (L.lgx_fill_normal(t.data_ptr(), t.numel(), float(std), sd, _dtype_code(t), _stream_ptr(t.device))
+          if first == 0 else
+          L.lgx_fill_normal_at(t.data_ptr(), int(first), t.numel(), float(std), sd, _dtype_code(t),
+                               _stream_ptr(t.device)))
+    _lib.check(rc, "lgx_fill_normal")
     return t
 
 

@@ -69,7 +69,8 @@ def test_lgx_csr_struct_layout_matches_header(tmp_path):
 
 
 # the kernels bench.py times and the f4 label walk: their state stays in registers
-HOT_KERNELS = ("spmm_segments", "spmm_fixup", "score_topk_bf16_lds", "score_topk_f32_lds", "score_topk_finalize",
+HOT_KERNELS = ("spmm_segments", "spmm_fixup", "score_topk_bf16_lds", "score_topk_f32_lds", "score_topk_f32_pc",
+               "score_topk_finalize",
                "strat_label_lds", "layer_epilogue", "score_dense_lds", "sum_slabs_kernel")
 
 

@@ -75,7 +75,8 @@ def test_f32_eight_waves_only_where_they_do_not_split():
     """d <= 128: 256-user workgroups, unless halving the user tiles alone would turn a single catalog
     sweep into a split launch -- then the 4-wave walk without splits (the Gowalla shape)."""
     gow = ops.score_topk_plan(27_522, 40_981, 64, torch.float32, 20)
-    assert gow.startswith("score_topk_f32_lds<4 waves, 64-item tiles, 16x16x4> users[0,27522) full-sweep") and \
+    assert gow.startswith("score_topk_f32_lds<4 waves + 4 producers, 64-item tiles, 16x16x4> users[0,27522) "
+                          "full-sweep") and \
         "n_splits=1" in gow and ";" not in gow, gow
     amz = ops.score_topk_plan(52_643, 91_599, 128, torch.float32, 20)
     assert amz == "score_topk_f32_lds<8 waves, 64-item tiles, 16x16x4> users[0,52643) full-sweep n_splits=1 utiles=206", amz
@@ -168,3 +169,40 @@ def test_score_minmax_vs_float64(dtype, B, I, d, rows):
         S = Qs[u0:u0 + 2048].double() @ items.double().T
         lo, hi = min(lo, S.min().item()), max(hi, S.max().item())
     assert abs(mm[0] - lo) <= 1e-5 * abs(lo) + 1e-6 and abs(mm[1] - hi) <= 1e-5 * abs(hi) + 1e-6, (mm, lo, hi)
+
+
+@pytest.mark.parametrize("B,I,k,rows", [(30_001, 33_333, 7, True), (26_000, 20_011, 24, False),
+                                        (28_123, 41_000, 1, True), (27_522, 40_981, 20, False)])
+def test_f32_producer_consumer_walk_equals_the_four_wave_walk(B, I, k, rows):
+    """fp32 d = 64 with a 128-user tile plan (the Gowalla shape's): the producer / consumer walk
+    (4 MFMA waves hand their scores through LDS to 4 top-k waves) against the 4-wave walk of the min/max
+    variant on the same inputs -- lists equal as sets with their values, bit for bit.  Padding users,
+    a catalog tail, user_rows, k = 1 / 7 / 20 / 24 (the largest whose lists fit beside the score
+    buffers; k = 32 keeps the 4-wave walk), and masks that take out each user's best items
+    (exact searches and parked suspects) plus random ones."""
+    d = 64
+    plan = ops.score_topk_plan(B, I, d, torch.float32, k)
+    assert plan.startswith("score_topk_f32_lds<4 waves + 4 producers") and "n_splits=1" in plan, plan
+    assert ops.score_topk_plan(B, I, d, torch.float32, 32).startswith("score_topk_f32_lds<4 waves, ")
+    g = torch.Generator(device=DEV).manual_seed(B + k)
+    n_q = B + 777 if rows else B
+    Q = torch.randn(n_q, d, device=DEV, generator=g) / 8
+    items = torch.randn(I, d, device=DEV, generator=g) / 8
+    user_rows = torch.randperm(n_q, device=DEV, generator=g)[:B] if rows else None
+    Qu = Q[user_rows] if rows else Q
+    best = torch.cat([torch.topk(Qu[u0:u0 + 2048] @ items.T, 40, dim=1).indices for u0 in range(0, B, 2048)])
+    m = torch.cat([best[:, ::2], torch.randint(0, I, (B, 30), device=DEV, generator=g)], 1).sort(1).values
+    keep = torch.ones_like(m, dtype=torch.bool)
+    keep[:, 1:] = m[:, 1:] != m[:, :-1]
+    indptr = torch.zeros(B + 1, dtype=torch.int64, device=DEV)
+    indptr[1:] = torch.cumsum(keep.sum(1), 0)
+    mask = (indptr, m[keep].to(torch.int32))
+    idx, val = lgx.score_topk(Q, items, k, user_rows=user_rows, mask=mask)
+    idx1, val1, _ = lgx.score_topk(Q, items, k, user_rows=user_rows, mask=mask, want_minmax=True)
+    ka, kb = torch.sort(idx.long(), 1), torch.sort(idx1.long(), 1)
+    assert torch.equal(ka.values, kb.values), "producer/consumer lists differ from the 4-wave walk"
+    assert torch.equal(val.gather(1, ka.indices), val1.gather(1, kb.indices))
+    assert (idx >= 0).all()
+    users = torch.repeat_interleave(torch.arange(B, device=DEV), indptr[1:] - indptr[:-1])
+    got = torch.arange(B, device=DEV)[:, None] * I + idx.long()
+    assert not torch.isin(got, users * I + mask[1].long()).any(), "a masked item was returned"

@@ -18,7 +18,10 @@ LAB = os.path.join(ROOT, "tools", "_ab", "lab")
 # [index, name] of the per-wave sums (tools/score_stats.py reads the same list)
 FIELDS = ["waves", "tiles", "cyc_loop", "cyc_stage", "cyc_epi_late", "cyc_compute", "cyc_epi_early", "cyc_wait",
           "n_fast", "n_defer", "n_full", "cyc_full", "cyc_flush", "n_event_tiles", "cyc_detect", "cyc_defer",
-          "cyc_dropmasked", "cyc_drain_ins", "cyc_insert_now", "n_unbounded", "n_rescan", "n_drain_steps"]
+          "cyc_dropmasked", "cyc_drain_ins", "cyc_insert_now", "n_unbounded", "n_rescan", "n_drain_steps",
+          # producer / consumer walk (PC): the producers' score writes, refill + MFMA issue, vmcnt wait and
+          # barrier wait, the consumers' barrier wait (the consumers' epilogue is cyc_epi_early)
+          "pc_waves", "cyc_pc_write", "cyc_pc_compute", "cyc_pc_vm", "cyc_pc_pwait", "cyc_pc_cwait"]
 
 
 def patch(src: str) -> str:
@@ -48,15 +51,41 @@ def patch(src: str) -> str:
         "            sync_from(ph);\n        }\n        refresh_tau();\n        lab_in += __builtin_amdgcn_s_memtime() - I0;\n    }\n\n    template <bool MINMAX>")
     rep("        } else {\n        }\n        drain(a);", "        } else {\n            ++lab_unb;\n        }\n        drain(a);")
     # per-wave accumulators at the loop
-    rep("    const bool stage_after = STAGGER && !late;  // wave-uniform\n    for (int64_t t = 0; t < ntiles; ++t) {\n"
+    # the producer / consumer loop
+    rep("            if (producer) {\n                if (t > 0 && t <= ntiles) {\n",
+        "            const unsigned long long P0 = __builtin_amdgcn_s_memtime();\n"
+        "            if (producer) {\n                if (t > 0 && t <= ntiles) {\n")
+    rep("                if (t < ntiles) {\n                    if (t + ahead < ntiles) stage(sbuf, tile_start(t + ahead));\n"
+        "                    compute_into(cur);\n                }\n",
+        "                const unsigned long long P1 = __builtin_amdgcn_s_memtime();\n"
+        "                if (t < ntiles) {\n                    if (t + ahead < ntiles) stage(sbuf, tile_start(t + ahead));\n"
+        "                    compute_into(cur);\n                }\n"
+        "                const unsigned long long P2 = __builtin_amdgcn_s_memtime();\n"
+        "                L_pc_write += P1 - P0; L_pc_compute += P2 - P1;\n")
+    rep("                epilogue(tile_start(t - 2));\n            }\n            __syncthreads();\n",
+        "                epilogue(tile_start(t - 2));\n                ++L_tiles;\n"
+        "                L_epi_early += __builtin_amdgcn_s_memtime() - P0;\n            }\n"
+        "            const unsigned long long PB = __builtin_amdgcn_s_memtime();\n"
+        "            if (producer) L_pc_vm += PB - P0 - 0;\n"
+        "            __syncthreads();\n"
+        "            if (producer) L_pc_pwait += __builtin_amdgcn_s_memtime() - PB; else L_pc_cwait += __builtin_amdgcn_s_memtime() - PB;\n")
+    rep("        if (producer) return;\n    } else\n",
+        "        if (producer) {\n            if (lane == 0) {\n"
+        "                atomicAdd(&g_lab[22], 1ull); atomicAdd(&g_lab[23], L_pc_write); atomicAdd(&g_lab[24], L_pc_compute);\n"
+        "                atomicAdd(&g_lab[25], L_pc_vm - L_pc_write - L_pc_compute); atomicAdd(&g_lab[26], L_pc_pwait);\n"
+        "            }\n            return;\n        }\n    } else\n")
+    rep("    const bool stage_after = STAGGER && !late;  // wave-uniform\n",
+        "    const bool stage_after = STAGGER && !late;  // wave-uniform\n"
+        "    unsigned long long L_loop0 = __builtin_amdgcn_s_memtime();\n"
+        "    unsigned long long L_pc_write = 0, L_pc_compute = 0, L_pc_vm = 0, L_pc_pwait = 0, L_pc_cwait = 0;\n")
+    rep("    } else\n    for (int64_t t = 0; t < ntiles; ++t) {\n"
         "        const int64_t t0 = tile_start(t);\n"
         "        if (!stage_after && t + ahead < ntiles) stage(sbuf, tile_start(t + ahead));\n"
         "        if (late && t > 0) epilogue(prev_t0);\n"
         "        compute();\n"
         "        if (stage_after && t + ahead < ntiles) stage(sbuf, tile_start(t + ahead));\n"
         "        if (!late) epilogue(t0);\n",
-        "    const bool stage_after = STAGGER && !late;  // wave-uniform\n"
-        "    unsigned long long L_loop0 = __builtin_amdgcn_s_memtime();\n"
+        "    } else\n"
         "    for (int64_t t = 0; t < ntiles; ++t) {\n"
         "        const int64_t t0 = tile_start(t);\n"
         "        const unsigned long long T0 = __builtin_amdgcn_s_memtime();\n"
@@ -114,6 +143,7 @@ def patch(src: str) -> str:
         "                                          L_wait, L_fast, L_defer, L_full, L_cyc_full, L_flush, L_ev, L_detect,\n"
         "                                          L_defer_cyc, st.lab_dm, st.lab_dr, st.lab_in, st.lab_unb, resc, st.lab_steps};\n"
         "        for (int j = 0; j < 22; ++j) atomicAdd(&g_lab[j], v[j]);\n"
+        "        atomicAdd(&g_lab[27], L_pc_cwait);\n"
         "    }\n"
         "}\n\ntemplate <int KSTEPS, bool MINMAX, int MODE = kTopK>")
     src += ("\nextern \"C\" int lgx_lab_stats(unsigned long long* out, int reset) {\n"

@@ -18,6 +18,7 @@ if "--lib" in sys.argv:
     j = sys.argv.index("--lib")
     _lib.LIB_PATH = os.path.abspath(sys.argv[j + 1])
     _lib._lib = None
+    _lib.ALLOW_MISSING = True
     del sys.argv[j:j + 2]
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 262144

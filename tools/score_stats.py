@@ -19,7 +19,8 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 sys.path.insert(0, ROOT)
 from factors_of_serendipity_recommendation_amd import _lib  # noqa: E402
 
-_lib.LIB_PATH = os.path.join(ROOT, "tools", "_ab", "lab", "factors_of_serendipity_recommendation_amd", "liblgx.so")
+_lib.LIB_PATH = os.environ.get("LGX_LAB_LIB") or os.path.join(ROOT, "tools", "_ab", "lab", "factors_of_serendipity_recommendation_amd",
+                                                               "liblgx.so")
 _lib._lib = None
 _lib.ALLOW_MISSING = True
 import make_stats_lab  # noqa: E402
@@ -55,6 +56,10 @@ def stats(fn, label):
     print("   per wave-tile: " + ", ".join(f"{k[2:]} {x:.3f}" for k, x in frac.items())
           + f"; cycles per full path {full_cyc:.0f}; flush {v['cyc_flush'] / max(1, v['waves']):.0f} per wave; "
             f"detect (incl. the MFMA results' wait) {det:.0f} per wave-tile; deferred path {dfr:.0f} per deferral", flush=True)
+    if v.get("pc_waves"):
+        print(f"   producer/consumer: producers per tile: score writes {v['cyc_pc_write'] / wt:.0f}, refill + MFMA issue "
+              f"{v['cyc_pc_compute'] / wt:.0f}, vmcnt {v['cyc_pc_vm'] / wt:.0f}, barrier {v['cyc_pc_pwait'] / wt:.0f}; "
+              f"consumers: epilogue {per['cyc_epi_early']:.0f}, barrier {v['cyc_pc_cwait'] / wt:.0f}", flush=True)
     nf = max(1, v["n_full"])
     print(f"   per full path: drop_masked {v['cyc_dropmasked'] / nf:.0f}, drain inserts {v['cyc_drain_ins'] / nf:.0f}, "
           f"direct inserts {v['cyc_insert_now'] / nf:.0f} cycles (flush included); unbounded {v['n_unbounded'] / nf:.3f}; "
