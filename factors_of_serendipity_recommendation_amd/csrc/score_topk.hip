@@ -1136,10 +1136,11 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
         // slot s of pair uwave: 8 lane-linear 16-B chunks per lane, c[ub][ib] at chunk 4 ub + ib
         auto slot = [&](int64_t t) { return sbuf_pc + ((size_t)uwave * 2 + (size_t)(t & 1)) * kPcScoreSlot + lane * 16; };
         // producer: tile t into one register set while the other (tile t - 1, its MFMAs issued an
-        // iteration ago) goes to the score buffer -- no wait on this tile's MFMAs before the barrier
-        f32x4 cA[2][4], cB[2][4];
-        auto iter = [&](int64_t t, f32x4 (&cur)[2][4], f32x4 (&prev)[2][4]) {
-            if (producer) {
+        // iteration ago) goes to the score buffer -- no wait on this tile's MFMAs before the barrier.
+        // The two roles run separate loops with the same barrier count, so their registers overlap.
+        if (producer) {
+            f32x4 cA[2][4], cB[2][4];
+            auto iter = [&](int64_t t, f32x4 (&cur)[2][4], f32x4 (&prev)[2][4]) {
                 if (t > 0 && t <= ntiles) {
                     unsigned char* sp = slot(t - 1);
 #pragma unroll
@@ -1153,7 +1154,18 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
                     compute_into(cur);
                 }
                 wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(t + ahead, ntiles - 1) - (t + 1)));
-            } else if (t >= 2) {  // tile t - 2, published by the previous barrier
+                __syncthreads();
+                buf = buf + 1 == nbuf ? 0 : buf + 1;
+                sbuf = sbuf + 1 == nbuf ? 0 : sbuf + 1;
+            };
+            for (int64_t t = 0; t < ntiles + 2; t += 2) {
+                iter(t, cA, cB);
+                if (t + 1 < ntiles + 2) iter(t + 1, cB, cA);
+            }
+            return;
+        }
+        for (int64_t t = 0; t < ntiles + 2; ++t) {
+            if (t >= 2) {  // tile t - 2, published by the previous barrier
                 const unsigned char* sp = slot(t - 2);
 #pragma unroll
                 for (int ub = 0; ub < 2; ++ub)
@@ -1162,14 +1174,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
                 epilogue(tile_start(t - 2));
             }
             __syncthreads();
-            buf = buf + 1 == nbuf ? 0 : buf + 1;
-            sbuf = sbuf + 1 == nbuf ? 0 : sbuf + 1;
-        };
-        for (int64_t t = 0; t < ntiles + 2; t += 2) {
-            iter(t, cA, cB);
-            if (t + 1 < ntiles + 2) iter(t + 1, cB, cA);
         }
-        if (producer) return;
     } else
     for (int64_t t = 0; t < ntiles; ++t) {
         const int64_t t0 = tile_start(t);
