@@ -111,3 +111,18 @@ def test_sharded_propagation_world1_rccl_forced_collectives(K, dt):
     p.join(timeout=120)
     assert ok, info
     assert p.exitcode == 0
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_fill_normal_rows_equal_rows_of_the_full_table(dt):
+    """lgx_fill_normal_at (bench.py N>1: each rank fills only its own rows of E0): rows [r0, r1) of a
+    table filled from offset r0 * d equal the same rows of the whole table, bit for bit, for odd
+    offsets (the Box-Muller pairs straddle the cut) as well."""
+    import factors_of_serendipity_recommendation_amd as lgx
+    N, d = 10_001, 24
+    full = lgx.fill_normal((N, d), 0.1, 2020, dtype=dt)
+    for r0, r1 in ((0, 1), (1, 2), (3_333, 7_777), (N - 5, N)):
+        part = lgx.fill_normal((r1 - r0, d), 0.1, 2020, dtype=dt, first=r0 * d)
+        assert torch.equal(part, full[r0:r1]), (r0, r1)
+    flat = lgx.fill_normal((7,), 0.1, 2020, dtype=dt, first=5)  # an odd element offset
+    assert torch.equal(flat, full.view(-1)[5:12])
