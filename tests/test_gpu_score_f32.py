@@ -172,13 +172,15 @@ def test_score_minmax_vs_float64(dtype, B, I, d, rows):
 
 
 @pytest.mark.parametrize("B,I,k,rows", [(30_001, 33_333, 7, True), (26_000, 20_011, 24, False),
-                                        (28_123, 41_000, 1, True), (27_522, 40_981, 20, False)])
+                                        (28_123, 41_000, 1, True), (27_522, 40_981, 20, False),
+                                        (40_000, 300_000, 20, True)])
 def test_f32_producer_consumer_walk_equals_the_four_wave_walk(B, I, k, rows):
     """fp32 d = 64 with a 128-user tile plan (the Gowalla shape's): the producer / consumer walk
     (4 MFMA waves hand their scores through LDS to 4 top-k waves) against the 4-wave walk of the min/max
     variant on the same inputs -- lists equal as sets with their values, bit for bit.  Padding users,
     a catalog tail, user_rows, k = 1 / 7 / 20 / 24 (the largest whose lists fit beside the score
-    buffers; k = 32 keeps the 4-wave walk), and masks that take out each user's best items
+    buffers; k = 32 keeps the 4-wave walk), a 300 K-item catalog swept in seeded stages (each stage's
+    lists seed the next) with a split tail range, and masks that take out each user's best items
     (exact searches and parked suspects) plus random ones."""
     d = 64
     plan = ops.score_topk_plan(B, I, d, torch.float32, k)
