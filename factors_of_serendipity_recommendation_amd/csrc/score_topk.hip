@@ -172,7 +172,10 @@ __device__ __forceinline__ uint32_t other_half(uint32_t x) {
 // The lane mirrors the worst kept entry (tau, tau_i) for the per-score filter.  An accepted
 // candidate overwrites the worst entry and the new worst is found by one scan of k independent
 // LDS reads -- no dependent shift chain.  Lists are sorted only when merged.
-template <int PEND>
+// REDEFER: after a drain, the block that overran a lane's slots is deferred again against the drained
+// lists before any direct insert (the fp32 walks with 12-16 slots per lane: Amazon-book shape 14.13 ->
+// 13.78 ms; with 4 slots, fp32 at d = 256, it costs 4.5 %, and bf16 C5 0.6 %: profiles/r06_pc_variants_ab.txt)
+template <int PEND, bool REDEFER = false>
 struct WaveTopKT {
     uint64_t* keys;  // this lane's user: [k]
     int k, h;
@@ -400,9 +403,11 @@ struct WaveTopKT {
         // unconditional 8-B LDS write to slot min(n, kPend) and n += (score >= tau) -- so an event
         // costs a few instructions per score whatever the lanes do.  Ties at tau and masked items are
         // sorted out when the slots are drained (exact key compare, mask test).  A lane that runs past
-        // its slots (n > kPend) sends the whole block down the exact path instead: drain, then insert
-        // every survivor directly.  An unbounded filter takes that path too.
-        if (__ballot(unbounded()) == 0ull) {
+        // its slots (n > kPend) drains every lane's slots; with REDEFER the block is then deferred again
+        // against the drained lists (their thresholds rose, the slots are empty), and only a lane that
+        // overruns them still sends the block down the exact path: insert every survivor directly.  An
+        // unbounded filter takes that path too.
+        auto defer = [&]() -> bool {
             int n = pcnt;
 #pragma unroll
             for (int q = 0; q < 2 * NACC; ++q) {
@@ -416,13 +421,13 @@ struct WaveTopKT {
                     n += sc >= tau ? 1 : 0;
                 }
             }
-            if (__ballot(n > kPend) == 0ull) {
-                pcnt = n;
-                return;
-            }
-        } else {
-        }
+            if (__ballot(n > kPend) != 0ull) return false;
+            pcnt = n;
+            return true;
+        };
+        if (__ballot(unbounded()) == 0ull && defer()) return;
         drain(a);
+        if (REDEFER && __ballot(unbounded()) == 0ull && defer()) return;
         insert_now<NACC, L16>(a, acc0, acc1, ib, survivors<NACC, L16>(acc0, acc1, ib, rem));
     }
 
@@ -826,7 +831,7 @@ __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreAr
     const int h = lane >> 5, col = lane & 31;
     const bool producer = PC && wave >= UW;  // wave-uniform
     const int uwave = PC ? wave % UW : wave;  // the user block of this wave (its pair's, PC)
-    typedef WaveTopKT<lds_pend(F32, KSTEPS, PC ? UW : WAVES)> TopK;
+    typedef WaveTopKT<lds_pend(F32, KSTEPS, PC ? UW : WAVES), F32 && KSTEPS <= 8> TopK;
     unsigned char* sbuf_pc = smem + (size_t)nbuf * G::TILE;  // PC: [UW pairs][2 slots][kPcScoreSlot]
     uint64_t* lk = reinterpret_cast<uint64_t*>(sbuf_pc + (PC ? (size_t)UW * 2 * kPcScoreSlot : 0) +
                                                (size_t)uwave * list_bytes_per_wave(k, TopK::kPend));
