@@ -49,12 +49,15 @@ def patch(src: str) -> str:
         "                                               uint32_t cmask) {\n        const unsigned long long I0 = __builtin_amdgcn_s_memtime();\n")
     rep("            sync_from(ph);\n        }\n        refresh_tau();\n    }\n\n    template <bool MINMAX>",
         "            sync_from(ph);\n        }\n        refresh_tau();\n        lab_in += __builtin_amdgcn_s_memtime() - I0;\n    }\n\n    template <bool MINMAX>")
-    rep("        } else {\n        }\n        drain(a);", "        } else {\n            ++lab_unb;\n        }\n        drain(a);")
+    rep("        if (__ballot(unbounded()) == 0ull && defer()) return;\n        drain(a);",
+        "        if (__ballot(unbounded()) == 0ull && defer()) return;\n"
+        "        if (__ballot(unbounded()) != 0ull) ++lab_unb;\n        drain(a);")
     # per-wave accumulators at the loop
-    # the producer / consumer loop
-    rep("            if (producer) {\n                if (t > 0 && t <= ntiles) {\n",
-        "            const unsigned long long P0 = __builtin_amdgcn_s_memtime();\n"
-        "            if (producer) {\n                if (t > 0 && t <= ntiles) {\n")
+    # the producer / consumer loops (separate loops, same barrier count)
+    rep("            auto iter = [&](int64_t t, f32x4 (&cur)[2][4], f32x4 (&prev)[2][4]) {\n                if (t > 0 && t <= ntiles) {\n",
+        "            auto iter = [&](int64_t t, f32x4 (&cur)[2][4], f32x4 (&prev)[2][4]) {\n"
+        "                const unsigned long long P0 = __builtin_amdgcn_s_memtime();\n"
+        "                if (t > 0 && t <= ntiles) {\n")
     rep("                if (t < ntiles) {\n                    if (t + ahead < ntiles) stage(sbuf, tile_start(t + ahead));\n"
         "                    compute_into(cur);\n                }\n",
         "                const unsigned long long P1 = __builtin_amdgcn_s_memtime();\n"
@@ -62,18 +65,29 @@ def patch(src: str) -> str:
         "                    compute_into(cur);\n                }\n"
         "                const unsigned long long P2 = __builtin_amdgcn_s_memtime();\n"
         "                L_pc_write += P1 - P0; L_pc_compute += P2 - P1;\n")
-    rep("                epilogue(tile_start(t - 2));\n            }\n            __syncthreads();\n",
-        "                epilogue(tile_start(t - 2));\n                ++L_tiles;\n"
-        "                L_epi_early += __builtin_amdgcn_s_memtime() - P0;\n            }\n"
-        "            const unsigned long long PB = __builtin_amdgcn_s_memtime();\n"
-        "            if (producer) L_pc_vm += PB - P0 - 0;\n"
-        "            __syncthreads();\n"
-        "            if (producer) L_pc_pwait += __builtin_amdgcn_s_memtime() - PB; else L_pc_cwait += __builtin_amdgcn_s_memtime() - PB;\n")
-    rep("        if (producer) return;\n    } else\n",
-        "        if (producer) {\n            if (lane == 0) {\n"
+    rep("                wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(t + ahead, ntiles - 1) - (t + 1)));\n"
+        "                __syncthreads();\n                buf = buf + 1 == nbuf ? 0 : buf + 1;\n",
+        "                wait_vmcnt_le(my_pieces * (int)max<int64_t>(0, min<int64_t>(t + ahead, ntiles - 1) - (t + 1)));\n"
+        "                const unsigned long long PB = __builtin_amdgcn_s_memtime();\n"
+        "                L_pc_vm += PB - P0;\n"
+        "                __syncthreads();\n"
+        "                L_pc_pwait += __builtin_amdgcn_s_memtime() - PB;\n"
+        "                buf = buf + 1 == nbuf ? 0 : buf + 1;\n")
+    rep("                if (t + 1 < ntiles + 2) iter(t + 1, cB, cA);\n            }\n            return;\n",
+        "                if (t + 1 < ntiles + 2) iter(t + 1, cB, cA);\n            }\n"
+        "            if (lane == 0) {\n"
         "                atomicAdd(&g_lab[22], 1ull); atomicAdd(&g_lab[23], L_pc_write); atomicAdd(&g_lab[24], L_pc_compute);\n"
         "                atomicAdd(&g_lab[25], L_pc_vm - L_pc_write - L_pc_compute); atomicAdd(&g_lab[26], L_pc_pwait);\n"
-        "            }\n            return;\n        }\n    } else\n")
+        "            }\n            return;\n")
+    rep("            if (t >= 2) {  // tile t - 2, published by the previous barrier\n",
+        "            const unsigned long long C0 = __builtin_amdgcn_s_memtime();\n"
+        "            if (t >= 2) {  // tile t - 2, published by the previous barrier\n")
+    rep("                epilogue(tile_start(t - 2));\n            }\n            __syncthreads();\n        }\n",
+        "                epilogue(tile_start(t - 2));\n                ++L_tiles;\n"
+        "                L_epi_early += __builtin_amdgcn_s_memtime() - C0;\n            }\n"
+        "            const unsigned long long CB = __builtin_amdgcn_s_memtime();\n"
+        "            __syncthreads();\n"
+        "            L_pc_cwait += __builtin_amdgcn_s_memtime() - CB;\n        }\n")
     rep("    const bool stage_after = STAGGER && !late;  // wave-uniform\n",
         "    const bool stage_after = STAGGER && !late;  // wave-uniform\n"
         "    unsigned long long L_loop0 = __builtin_amdgcn_s_memtime();\n"
