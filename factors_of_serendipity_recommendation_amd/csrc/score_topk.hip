@@ -807,7 +807,7 @@ constexpr int kF32LdsWaves = 4;
 // to its consumer through an LDS score buffer (two slots per pair), and the consumer runs the top-k
 // epilogue, the mask and the exact path -- so a tile's events run on the SIMD beside the next tile's
 // MFMAs instead of after them.  One workgroup barrier per tile: producer p writes tile t - 1's scores
-// while it has tile t's MFMAs in flight, consumer p ranks tile t - 2.  SCORE_SLOT bytes per slot.
+// while it has tile t's MFMAs in flight, consumer p ranks tile t - 2.  kPcScoreSlot bytes per slot.
 constexpr int kPcScoreSlot = 8 * 1024;
 template <int DT, int KSTEPS, bool MINMAX, int MODE, int WAVES, int NACC, bool STAGGER, bool PC = false>
 __device__ __forceinline__ void score_topk_lds_body(unsigned char* smem, ScoreArgs a, int xcd_affine,
