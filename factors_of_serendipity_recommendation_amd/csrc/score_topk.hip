@@ -1938,7 +1938,8 @@ int launch_f32_lds_kernel(const ScoreArgs& a, const SplitPlan& p, hipStream_t st
     return LGX_OK;
 }
 
-// the producer / consumer walk replaces the 4-wave fp32 walk at d = 64 (the top-k sweep)
+// the producer / consumer walk replaces the 4-wave fp32 walk at d = 64: the top-k sweep and, since
+// the roles run separate loops (no spill), its floor pass (Gowalla route 2.77 -> 2.66 ms, r06w)
 // where two ring tiles, the score buffers and the 4 consumers' lists fit the LDS (k <= 24 at 16 slots)
 inline bool f32_pc(const SplitPlan& p, int64_t d, int k, bool mm) {
     return p.waves == kF32LdsWaves && d == 64 && !mm &&
@@ -1979,7 +1980,7 @@ int launch_lds(const ScoreArgs& a, const SplitPlan& p, hipStream_t stream, int d
                         return LGX_ERR_UNSUPPORTED;
                 }
             }
-            if constexpr (!MM && MODE == kTopK)  // the floor pass keeps the 4-wave walk (its maxima spill here)
+            if constexpr (!MM && MODE != kMinMaxOnly)  // the top-k sweep and its floor pass
                 if (f32_pc(p, a.d, a.k, MM)) return launch_f32_pc_kernel<4, MODE>(a, p, stream);
             switch (ksteps) {
                 case 4: return launch_f32_lds_kernel<4, MM, MODE>(a, p, stream);
